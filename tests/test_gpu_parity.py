@@ -1,0 +1,349 @@
+"""HIP engine parity (gpu marker): the product path — yuma_simulation on
+libyuma_hip.so through the C-ABI — against the reference goldens and the CPU
+oracle. Bit-exact for discrete outputs (consensus levels, clip decisions,
+dividend-sheet CSV text); <= 1e-5 relative for fp32 values."""
+
+import hashlib
+import io
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN, assert_close
+from golden import specs
+from oracle import yuma_oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+from yuma_simulation._internal import engine, synth  # noqa: E402
+from yuma_simulation._internal import yumas as Y  # noqa: E402
+from yuma_simulation._internal.cases import BaseCase, cases  # noqa: E402
+from yuma_simulation._internal.simulation_utils import (  # noqa: E402
+    SimulationRun,
+    generate_total_dividends_table,
+    run_simulation,
+    run_simulations,
+)
+
+FN = {"rust": Y.YumaRust, "yuma1": Y.Yuma, "yuma2": Y.Yuma2, "yuma3": Y.Yuma3, "yuma4": Y.Yuma4}
+VARIANT_ID = {"rust": engine.VARIANT_RUST, "yuma1": engine.VARIANT_YUMA1, "yuma2": engine.VARIANT_YUMA2,
+              "yuma3": engine.VARIANT_YUMA3, "yuma4": engine.VARIANT_YUMA4}
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    assert torch.cuda.is_available(), "gpu tests need a ROCm GPU"
+    engine.load_library()  # fails loudly if the HIP library is missing
+    yield
+
+
+def config_from(spec):
+    sim, par = specs.split_spec(spec)
+    return Y.YumaConfig(simulation=Y.SimulationHyperparameters(**sim), yuma_params=Y.YumaParams(**par))
+
+
+def call(variant, W, S, B_old, cfg, W_prev=None):
+    if variant == "yuma2":
+        return FN[variant](W, W_prev, S, B_old, cfg)
+    return FN[variant](W, S, B_old, cfg)
+
+
+def state_of(variant, r):
+    return r["validator_bonds"] if variant in ("yuma3", "yuma4") else r["validator_ema_bond"]
+
+
+def to_np(x):
+    return x.detach().cpu().numpy() if isinstance(x, torch.Tensor) else np.asarray(x)
+
+
+# ---------------------------------------------------------------------------
+# dividend sheet (config 5) and the built-in cases (config 1)
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("bi", range(4))
+def test_sheet_csv_byte_identical(bi):
+    """generate_total_dividends_table -> CSV text equals the reference's."""
+    with open(os.path.join(GOLDEN, "sheet.json")) as f:
+        meta = json.load(f)
+    beta = specs.BETAS[bi]
+    versions = [(v, Y.YumaParams(**p)) for v, p in zip(specs.VERSIONS, specs.SHEET_PARAMS)]
+    df = generate_total_dividends_table(cases, versions, Y.SimulationHyperparameters(bond_penalty=beta))
+    buf = io.StringIO()
+    df.to_csv(buf, index=False, float_format="%.6f")
+    name = f"total_dividends_b{beta}.csv"
+    assert buf.getvalue() == meta["csv"][name]
+    assert hashlib.md5(buf.getvalue().encode()).hexdigest() == meta["csv_md5"][name]
+
+
+def test_sheet_runs_per_epoch(golden):
+    """Every (beta, case, version) run: consensus exact, dividends / bonds /
+    incentives within tolerance; all 504 runs go through batched launches."""
+    g = golden("sheet.npz")
+    runs, where = [], []
+    for bi, beta in enumerate(specs.BETAS):
+        for ci, case in enumerate(cases):
+            for vi, version in enumerate(specs.VERSIONS):
+                cfg = Y.YumaConfig(simulation=Y.SimulationHyperparameters(bond_penalty=beta),
+                                   yuma_params=Y.YumaParams(**specs.SHEET_PARAMS[vi]))
+                runs.append(SimulationRun(case, version, cfg))
+                where.append((bi, ci, vi))
+    results = run_simulations(runs)
+    for (bi, ci, vi), (div, bonds, inc) in zip(where, results):
+        case = cases[ci]
+        tag = f"b{specs.BETAS[bi]} {case.name[:7]} {specs.VERSIONS[vi]}"
+        d = np.array([div[v] for v in case.validators]).T
+        assert_close(d, g["dividends"][bi, ci, vi], what=tag + " dividends")
+        assert_close(np.stack([to_np(b) for b in bonds]), g["bonds"][bi, ci, vi], what=tag + " bonds")
+        assert_close(np.stack([to_np(x) for x in inc]), g["incentives"][bi, ci, vi], what=tag + " I")
+
+
+def test_run_simulation_single_case_matches(golden):
+    g = golden("sheet.npz")
+    cfg = Y.YumaConfig(simulation=Y.SimulationHyperparameters(bond_penalty=0.99))
+    div, bonds, inc = run_simulation(cases[10], "Yuma 1 (paper)", cfg)
+    d = np.array([div[v] for v in cases[10].validators]).T
+    assert_close(d, g["dividends"][2, 10, 1])
+    assert len(bonds) == 40 and bonds[0].device.type == "cpu"
+
+
+def test_invalid_version_raises():
+    with pytest.raises(ValueError, match="Invalid Yuma function."):
+        run_simulation(cases[0], "Yuma 7", Y.YumaConfig())
+
+
+# ---------------------------------------------------------------------------
+# single-epoch variant functions (full result dictionaries)
+# ---------------------------------------------------------------------------
+def _small_cases():
+    for iname in ("synth16x64", "rand16x64", "edge3x5"):
+        for variant in specs.VARIANTS:
+            for cname in specs.CONFIGS:
+                if cname.startswith("liquid") and variant == "yuma3":
+                    continue
+                yield iname, variant, cname
+
+
+@pytest.mark.parametrize("iname,variant,cname", list(_small_cases()))
+def test_epoch_functions_match_reference(golden, iname, variant, cname):
+    g = golden("epoch_small.npz")
+    cfg = config_from(specs.CONFIGS[cname])
+    W0, S0 = torch.from_numpy(g[f"in__{iname}__W0"]), torch.from_numpy(g[f"in__{iname}__S0"])
+    W1, S1 = torch.from_numpy(g[f"in__{iname}__W1"]), torch.from_numpy(g[f"in__{iname}__S1"])
+    r0 = call(variant, W0, S0, None, cfg)
+    prev = r0["weight"] if variant == "yuma2" else None
+    r1 = call(variant, W1, S1, state_of(variant, r0).clone(), cfg, W_prev=prev)
+    for step, r in (("e0", r0), ("e1", r1)):
+        tag = f"out__{iname}__{variant}__{cname}__{step}"
+        keys = [k[len(tag) + 2:] for k in g.files if k.startswith(tag + "__") and not k.endswith("__pyfloat")]
+        assert list(r) == [k for k in Y.RESULT_KEYS[VARIANT_ID[variant]]]
+        assert set(keys) == set(r)
+        for k in keys:
+            exp = g[f"{tag}__{k}"]
+            got = r[k]
+            if f"{tag}__{k}__pyfloat" in g.files:
+                assert isinstance(got, float), (tag, k)
+                assert got == float(exp) or (np.isnan(got) and np.isnan(exp))
+                continue
+            assert isinstance(got, torch.Tensor) and got.device.type == "cpu", (tag, k)
+            if k == "server_consensus_weight":
+                np.testing.assert_array_equal(to_np(got), exp, err_msg=f"{tag} {k}")
+            elif k == "consensus_clipped_weight":
+                # clip decisions: which entries were clipped must be identical
+                wsrc = r["weight"] if variant != "yuma2" or step == "e0" else prev
+                np.testing.assert_array_equal(to_np(got) < to_np(wsrc), exp < to_np(wsrc), err_msg=tag)
+                assert_close(to_np(got), exp, what=f"{tag} {k}")
+            else:
+                assert_close(to_np(got), exp, what=f"{tag} {k}")
+
+
+def test_yuma_alias_without_history():
+    W = torch.rand(8, 16)
+    S = torch.rand(8)
+    r = Y.Yuma(W, S)
+    assert r["validator_ema_bond"] is r["validator_bond"]
+    assert isinstance(r["bond_alpha"], float) and torch.isnan(r["alpha_a"])
+
+
+def test_epoch_on_gpu_tensors_stays_on_gpu():
+    W = torch.rand(8, 16, device="cuda")
+    S = torch.rand(8, device="cuda")
+    r = Y.Yuma3(W, S)
+    assert r["validator_bonds"].is_cuda
+
+
+# ---------------------------------------------------------------------------
+# multi-epoch runs on synthetic and random inputs (run_simulation path)
+# ---------------------------------------------------------------------------
+class ArrayCase(BaseCase):
+    def __init__(self, W, S, reset_epoch, reset_index):
+        names = [f"V{i}" for i in range(W.shape[1])]
+        super().__init__(name="synthetic", validators=names, base_validator=names[0], num_epochs=W.shape[0],
+                         reset_bonds=True, reset_bonds_index=reset_index, reset_bonds_epoch=reset_epoch)
+        self._W = [torch.from_numpy(w.copy()) for w in W]
+        self._S = [torch.from_numpy(s.copy()) for s in S]
+
+    @property
+    def weights_epochs(self):
+        return self._W
+
+    @property
+    def stakes_epochs(self):
+        return self._S
+
+
+@pytest.mark.parametrize("sname", ["synth64x512", "rand32x256"])
+def test_run_medium_matches_reference(golden, sname):
+    g = golden("run_medium.npz")
+    W, S = g[f"in__{sname}__W"], g[f"in__{sname}__S"]
+    re, ri = (int(x) for x in g[f"in__{sname}__reset"])
+    case = ArrayCase(W, S, re, ri)
+    for vi, version in enumerate(specs.VERSIONS):
+        cfg = Y.YumaConfig(simulation=Y.SimulationHyperparameters(bond_penalty=0.5),
+                           yuma_params=Y.YumaParams(**specs.SHEET_PARAMS[vi]))
+        div, bonds, inc = run_simulation(case, version, cfg)
+        tag = f"out__{sname}__{vi}"
+        d = np.array([div[v] for v in case.validators]).T
+        assert_close(d, g[f"{tag}__dividends"], what=f"{tag} dividends")
+        assert_close(to_np(bonds[-1]), g[f"{tag}__B_last"], what=f"{tag} B_last")
+        assert_close(to_np(bonds[0]), g[f"{tag}__B_first"], what=f"{tag} B_first")
+        assert_close(np.stack([to_np(b).astype(np.float64).sum(axis=0) for b in bonds]),
+                     g[f"{tag}__Bsum_epochs"], what=f"{tag} Bsum")
+        assert_close(np.stack([to_np(x) for x in inc]), g[f"{tag}__I"], what=f"{tag} I")
+
+
+# ---------------------------------------------------------------------------
+# BASELINE shape 256 x 4096
+# ---------------------------------------------------------------------------
+@pytest.fixture(scope="module")
+def large_inputs(golden):
+    g = golden("large.npz")
+    W = synth.weights(specs.LARGE_SEED, 2, 1, 256, 4096)[:, 0]
+    S = synth.stakes(specs.LARGE_SEED, 2, 1, 256)[:, 0]
+    return g, W, S
+
+
+@pytest.mark.parametrize("name", list(specs.LARGE_SPECS))
+def test_large_epoch_matches_reference(large_inputs, name):
+    g, W, S = large_inputs
+    variant = name.split("_")[0]
+    cfg = config_from(specs.LARGE_SPECS[name])
+    r0 = call(variant, torch.from_numpy(W[0]), torch.from_numpy(S[0]), None, cfg)
+    prev = r0["weight"] if variant == "yuma2" else None
+    r1 = call(variant, torch.from_numpy(W[1]), torch.from_numpy(S[1]), state_of(variant, r0).clone(), cfg,
+              W_prev=prev)
+    idx = g["sample_idx"]
+    for step, r in (("e0", r0), ("e1", r1)):
+        tag = f"out__{name}__{step}"
+        np.testing.assert_array_equal(to_np(r["server_consensus_weight"]), g[f"{tag}__server_consensus_weight"])
+        for k in ("server_incentive", "server_rank", "server_prerank", "validator_reward",
+                  "validator_reward_normalized"):
+            assert_close(to_np(r[k]), g[f"{tag}__{k}"], what=f"{tag} {k}")
+        B = to_np(state_of(variant, r))
+        assert_close(B.astype(np.float64).sum(axis=0), g[f"{tag}__B_colsum"], what=f"{tag} Bcol")
+        assert_close(B.astype(np.float64).sum(axis=1), g[f"{tag}__B_rowsum"], what=f"{tag} Brow")
+        assert_close(B[idx[:, 0], idx[:, 1]], g[f"{tag}__B_sample"], what=f"{tag} Bsample")
+        if f"{tag}__bond_alpha" in g.files:
+            assert_close(to_np(r["bond_alpha"]), g[f"{tag}__bond_alpha"], what=f"{tag} bond_alpha")
+
+
+def test_large_random_floats_decisions(golden):
+    g = golden("large.npz")
+    Wr, Sr = synth.random_float_inputs(int(g["rand__W_seed"]), 1, 256, 4096)
+    r = Y.Yuma(torch.from_numpy(Wr[0]), torch.from_numpy(Sr[0]))
+    np.testing.assert_array_equal(to_np(r["server_consensus_weight"]), g["rand__server_consensus_weight"])
+    assert_close(to_np(r["server_incentive"]), g["rand__server_incentive"])
+    assert_close(to_np(r["validator_reward_normalized"]), g["rand__validator_reward_normalized"])
+
+
+# ---------------------------------------------------------------------------
+# engine-level properties at full size (size-independent checks)
+# ---------------------------------------------------------------------------
+def test_device_synth_matches_numpy():
+    for (E, N, V, M) in ((2, 3, 17, 130), (1, 1, 256, 4096)):
+        d = engine.synth_weights(0xABCDEF, E, N, V, M, t0=5).cpu().numpy()
+        h = synth.weights(0xABCDEF, E, N, V, M, t0=5)
+        np.testing.assert_array_equal(d, h)
+
+
+@pytest.mark.parametrize("variant", list(VARIANT_ID))
+def test_multi_epoch_vs_oracle_and_chunk_invariance(variant):
+    """64 epochs at 256x4096: engine run == oracle loop (C exact, rest within
+    tolerance); and the result is bitwise independent of the chunking."""
+    E, V, M = 12, 256, 4096
+    W = synth.weights(0x5EED0002, E, 1, V, M)
+    S = synth.stakes(0x5EED0002, E, 1, V, period=5)
+    cfg = config_from({"liquid_alpha": True} if variant in ("yuma1", "yuma4") else {})
+    vid = VARIANT_ID[variant]
+    prm = [engine.make_params(vid, cfg)]
+    a = engine.run(vid, prm, torch.from_numpy(W), torch.from_numpy(S), want_hist=True, chunk_epochs=E)
+    b = engine.run(vid, prm, torch.from_numpy(W), torch.from_numpy(S), want_hist=True, chunk_epochs=5)
+    torch.cuda.synchronize()
+    assert torch.equal(a.B_hist, b.B_hist) and torch.equal(a.Dn, b.Dn) and torch.equal(a.C, b.C)
+    version = {"rust": "Yuma 0 (subtensor)", "yuma1": "Yuma 1 (paper) - liquid alpha on",
+               "yuma2": "Yuma 2 (Adrian-Fish)", "yuma3": "Yuma 3 (Rhef)",
+               "yuma4": "Yuma 4 (Rhef+relative bonds) - liquid alpha on"}[variant]
+    ref = orc.run(version, W[:, 0], S[:, 0], cfg)
+    np.testing.assert_array_equal(a.C[:, 0].cpu().numpy(), ref["C"])
+    assert_close(a.Dn[:, 0].cpu().numpy(), ref["Dn"], what="Dn")
+    assert_close(a.I[:, 0].cpu().numpy(), ref["I"], what="I")
+    assert_close(a.B_hist[:, 0].cpu().numpy(), ref["B"], what="B")
+    # properties: levels quantised, dividends normalised
+    lev = a.C.cpu().numpy() * 65535.0
+    assert np.allclose(lev, np.rint(lev), atol=1e-2)
+    assert np.allclose(a.Dn.sum(dim=-1).cpu().numpy(), 1.0, atol=1e-5)
+
+
+def test_batched_scenarios_equal_individual_runs():
+    """N scenarios in one launch == each alone (bitwise), params differing."""
+    E, N, V, M = 6, 5, 64, 1000  # M % 4 == 0 but not a multiple of 64
+    W = synth.weights(77, E, N, V, M)
+    S = synth.stakes(77, E, N, V, period=3)
+    cfgs = [config_from({"kappa": 0.3 + 0.1 * n, "liquid_alpha": n % 2 == 1}) for n in range(N)]
+    for vid in (engine.VARIANT_YUMA1, engine.VARIANT_YUMA4):
+        prm = [engine.make_params(vid, c) for c in cfgs]
+        full = engine.run(vid, prm, torch.from_numpy(W), torch.from_numpy(S), want_hist=True)
+        for n in range(N):
+            one = engine.run(vid, [prm[n]], torch.from_numpy(W[:, n:n + 1]), torch.from_numpy(S[:, n:n + 1]),
+                             want_hist=True)
+            assert torch.equal(full.B_hist[:, n], one.B_hist[:, 0])
+            assert torch.equal(full.Dn[:, n], one.Dn[:, 0])
+
+
+@pytest.mark.parametrize("V,M", [(1, 1), (3, 7), (33, 65), (1024, 96), (300, 130)])
+def test_ragged_shapes_vs_oracle(V, M):
+    """Odd sizes exercise the scalar (non-float4) path and padded tiles."""
+    rng = np.random.default_rng(V * 1000 + M)
+    E = 3
+    W = rng.random((E, V, M), dtype=np.float32)
+    W[:, :, 0] = 0.0
+    S = rng.random((E, V), dtype=np.float32) + np.float32(0.01)
+    for variant, version in (("yuma1", "Yuma 1 (paper)"), ("rust", "Yuma 0 (subtensor)"),
+                             ("yuma3", "Yuma 3 (Rhef)"), ("yuma4", "Yuma 4 (Rhef+relative bonds)"),
+                             ("yuma2", "Yuma 2 (Adrian-Fish)")):
+        vid = VARIANT_ID[variant]
+        cfg = Y.YumaConfig()
+        res = engine.run(vid, [engine.make_params(vid, cfg)], torch.from_numpy(W[:, None]),
+                         torch.from_numpy(S[:, None]), want_hist=True)
+        ref = orc.run(version, W, S, cfg)
+        np.testing.assert_array_equal(res.C[:, 0].cpu().numpy(), ref["C"], err_msg=f"{variant} {V}x{M}")
+        assert_close(res.Dn[:, 0].cpu().numpy(), ref["Dn"], rtol=1e-4, what=f"{variant} {V}x{M} Dn")
+        assert_close(res.B_hist[:, 0].cpu().numpy(), ref["B"], rtol=1e-4, what=f"{variant} {V}x{M} B")
+
+
+def test_rejects_too_many_validators():
+    with pytest.raises(engine.EngineError):
+        engine.run(engine.VARIANT_YUMA3, [engine.make_params(3, Y.YumaConfig())],
+                   torch.zeros(1, 1, 1025, 8), torch.ones(1, 1, 1025))
+
+
+def test_deterministic_repeat():
+    E, V, M = 4, 256, 4096
+    W = engine.synth_weights(3, E, 1, V, M)
+    S = torch.from_numpy(synth.stakes(3, E, 1, V)).cuda()
+    prm = [engine.make_params(engine.VARIANT_YUMA3, Y.YumaConfig())]
+    a = engine.run(engine.VARIANT_YUMA3, prm, W, S, want_hist=True)
+    b = engine.run(engine.VARIANT_YUMA3, prm, W, S, want_hist=True)
+    torch.cuda.synchronize()
+    assert torch.equal(a.B_hist, b.B_hist) and torch.equal(a.Dn, b.Dn)

@@ -1,0 +1,147 @@
+"""Host-side logic and the C-ABI library surface (CPU only, no compute calls)."""
+
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import ROOT
+from yuma_simulation._internal import cases as C
+from yuma_simulation._internal import engine, synth
+from yuma_simulation._internal import yumas as Y
+from yuma_simulation._internal.simulation_utils import VERSION_TABLE, resolve_version
+
+
+def header_functions():
+    text = open(os.path.join(ROOT, "include", "yuma_hip.h")).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(yuma_[a-z_]+)\s*\(", text)))
+
+
+def test_library_exports_every_header_symbol():
+    lib = engine.load_library()
+    names = header_functions()
+    assert set(names) == set(engine.EXPORTED_SYMBOLS), names
+    for name in names:
+        assert hasattr(lib, name), name
+    assert engine.version().startswith("yuma_hip")
+
+
+def test_params_struct_layout_matches_header():
+    # the header promises 128 bytes; offsets of the double block are 8-aligned
+    assert ctypes.sizeof(engine.YumaParamsC) == 128
+    assert engine.YumaParamsC.ln_num.offset == 80
+    assert ctypes.sizeof(engine.YumaOutputsC) == 8 * len(engine.OUTPUT_FIELDS)
+
+
+def test_workspace_bytes_monotone():
+    a = engine.workspace_bytes(3, 1, 10, 256, 4096, False)
+    b = engine.workspace_bytes(3, 1, 20, 256, 4096, False)
+    c = engine.workspace_bytes(3, 1, 10, 256, 4096, True)
+    assert 0 < a < b and a < c
+
+
+def test_compute_without_gpu_fails_loudly():
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(engine.EngineUnavailable):
+        Y.Yuma(torch.rand(4, 8), torch.rand(4))
+
+
+def test_config_defaults_and_flattening():
+    cfg = Y.YumaConfig()
+    assert (cfg.kappa, cfg.bond_penalty, cfg.total_epoch_emission) == (0.5, 1.0, 100.0)
+    assert (cfg.validator_emission_ratio, cfg.total_subnet_stake, cfg.consensus_precision) == (0.41, 1e6, 100_000)
+    assert (cfg.bond_alpha, cfg.liquid_alpha, cfg.alpha_high, cfg.alpha_low) == (0.1, False, 0.9, 0.7)
+    assert (cfg.decay_rate, cfg.capacity_alpha) == (0.1, 0.1)
+    assert cfg.override_consensus_high is None and cfg.override_consensus_low is None
+    cfg2 = Y.YumaConfig(simulation=Y.SimulationHyperparameters(kappa=0.7), yuma_params=Y.YumaParams(bond_alpha=0.3))
+    assert cfg2.kappa == 0.7 and cfg2.bond_alpha == 0.3
+
+
+def test_names_and_dispatch():
+    n = Y.YumaSimulationNames()
+    assert n.YUMA_RUST == "Yuma 0 (subtensor)" and n.YUMA4_LIQUID.endswith("liquid alpha on")
+    assert len(VERSION_TABLE) == 9
+    assert resolve_version(n.YUMA31) == (engine.VARIANT_YUMA3, engine.RESET_ALWAYS)
+    assert resolve_version(n.YUMA4) == (engine.VARIANT_YUMA4, engine.RESET_IF_ZERO_CONSENSUS)
+    with pytest.raises(ValueError, match="Invalid Yuma function."):
+        resolve_version("Yuma 5")
+
+
+def test_bisection_trip_count():
+    assert engine.bisect_iterations(100_000) == 17
+    assert engine.bisect_iterations(1000) == 10
+    assert engine.bisect_iterations(1) == 0
+    with pytest.raises(ZeroDivisionError):
+        engine.bisect_iterations(0)
+
+
+def test_param_rounding_follows_python_then_fp32():
+    cfg = Y.YumaConfig(simulation=Y.SimulationHyperparameters(kappa=0.3, bond_penalty=0.99),
+                       yuma_params=Y.YumaParams(bond_alpha=0.025, decay_rate=0.1))
+    p = engine.make_params(engine.VARIANT_YUMA4, cfg)
+    assert p.kappa == float(np.float32(0.3))
+    assert p.one_minus_bond_penalty == float(np.float32(1 - 0.99))
+    assert p.one_minus_bond_alpha == float(np.float32(1 - 0.025))
+    assert p.decay_keep == float(np.float32(0.9))
+    assert p.maxint == 2.0**64
+    assert p.liquid_mode == engine.LIQUID_OFF
+
+
+def test_liquid_override_modes():
+    mk = lambda **kw: engine.make_params(engine.VARIANT_YUMA1, Y.YumaConfig(yuma_params=Y.YumaParams(liquid_alpha=True, **kw)))
+    assert mk().liquid_mode == engine.LIQUID_QUANTILE and mk().override_flags == 0
+    p = mk(override_consensus_high=0.5)
+    assert p.override_flags == engine.OVR_HIGH
+    p = mk(override_consensus_high=0.5, override_consensus_low=0.5)
+    assert p.liquid_mode == engine.LIQUID_QUANTILE and p.override_flags & engine.OVR_FORCE_Q99
+    p = mk(override_consensus_high=0.5, override_consensus_low=0.1)
+    assert p.liquid_mode == engine.LIQUID_CONST_AB
+    a = (np.log(1 / 0.9 - 1) - np.log(1 / 0.7 - 1)) / (0.1 - 0.5)
+    assert p.const_a == float(np.float32(a))
+    # Yuma3 ignores liquid alpha entirely (reference yumas.py:399-491)
+    p3 = engine.make_params(engine.VARIANT_YUMA3, Y.YumaConfig(yuma_params=Y.YumaParams(liquid_alpha=True, alpha_high=1.0)))
+    assert p3.liquid_mode == engine.LIQUID_OFF
+    with pytest.raises(ValueError):  # math.log(0), as the reference raises
+        mk(alpha_high=1.0)
+
+
+def test_reset_without_metadata_never_fires():
+    p = engine.make_params(engine.VARIANT_YUMA3, Y.YumaConfig(), reset_mode=engine.RESET_ALWAYS)
+    assert p.reset_mode == engine.RESET_NONE
+
+
+def test_cases_surface():
+    assert len(C.cases) == 14 and list(C.class_registry) == [f"Case {i}" for i in range(1, 15)]
+    c1 = C.create_case("Case 1")
+    W = c1.weights_epochs
+    assert len(W) == 40 and W[1].tolist() == [[0.0, 1.0], [1.0, 0.0], [1.0, 0.0]]
+    assert c1.stakes_epochs[0].tolist() == pytest.approx([0.8, 0.1, 0.1])
+    c9 = C.create_case("Case 9")
+    assert c9.stakes_epochs[6].tolist() == pytest.approx([0.8, 0.2, 0.0])
+    assert C.create_case("Case 5").reset_bonds_epoch == 20
+    with pytest.raises(ValueError):
+        C.create_case("Case 99")
+    with pytest.raises(ValueError):
+        C.Case1(base_validator="nobody")
+    assert C.create_case("Case 1", num_epochs=7).packed_weights().shape == (7, 3, 2)
+    # the returned lists are copies: mutating one does not leak into the next access
+    W[0][0, 0] = 42.0
+    assert c1.weights_epochs[0][0, 0] == 1.0
+
+
+def test_synth_exactness_properties():
+    W = synth.weights(5, 2, 2, 64, 4096)
+    assert W.dtype == np.float32 and np.all(W == np.floor(W))
+    rs = W.astype(np.float64).sum(axis=-1)
+    assert rs.max() < 2**24 and rs.min() >= 32
+    S = synth.stakes(5, 3, 2, 64, period=2)
+    assert np.all(S.astype(np.int64).sum(axis=-1) == 2**20)
+    assert np.array_equal(S[0], S[1]) and not np.array_equal(S[1], S[2])
+    # deterministic and scenario-distinct
+    assert np.array_equal(W, synth.weights(5, 2, 2, 64, 4096))
+    assert not np.array_equal(W[:, 0], W[:, 1])

@@ -1,0 +1,1340 @@
+// yuma_engine.hip — MI355X (gfx950) engine for the Yuma consensus epoch step.
+//
+// What it computes: the epoch step of the reference's five variants
+// (src/yuma_simulation/_internal/yumas.py:61 YumaRust, :175 Yuma, :285 Yuma2,
+// :399 Yuma3, :494 Yuma4) and the epoch loop of run_simulation
+// (src/yuma_simulation/_internal/simulation_utils.py:26-112).
+//
+// How (DESIGN.md has the long form):
+//  * Fact 1 of the survey: inside one epoch everything except the bond
+//    recurrence is a pure function of (W_t, S_t). So phase 1 runs over ALL
+//    epochs of a chunk at once (one slice = one (epoch, scenario) matrix):
+//      k_rowsum     row sums of W + stake normalisation          (HBM pass 1)
+//      k_consensus  per 64-miner tile: normalise, prerank, the
+//                   kappa-bisection per column (LDS column reduce) (HBM pass 2)
+//      k_quantise   per slice: sum C, int32 quantisation, liquid-alpha
+//                   quantiles by integer histogram select, bond_alpha[m]
+//      k_rank       per tile: clip, rank R, sum-R partials       (HBM pass 3)
+//      k_incentive  per slice: I = nan_to_num(R / sum R)
+//  * Phase 2 (k_bonds*) walks the epochs of the chunk per bond tile with the
+//    bond state held in registers (fact 2: the recurrence is column-local),
+//    reading W_t once more (HBM pass 4) and writing per-tile dividend partials.
+//  * k_finalize turns the partials into D and D_normalized per slice.
+// No float atomics, no data-dependent reduction order: every sum is a fixed
+// tree, so results are bitwise reproducible run to run.
+//
+// Numerics follow the reference op by op in fp32 (torch CPU semantics): Python
+// scalars are rounded to fp32 before they meet a tensor, `py / t` is
+// reciprocal(t) * py, math.e ** t is pow(fp32(e), t), torch.quantile's lerp
+// uses an FMA, torch.min / clamp propagate NaN, nan_to_num maps +-inf to
+// +-FLT_MAX. Built with -ffp-contract=off and IEEE division so that no
+// product is fused unless the reference fuses it.
+#include <hip/hip_runtime.h>
+
+#include <float.h>
+#include <math.h>
+#include <stdarg.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "yuma_hip.h"
+
+#define YUMA_VERSION_STRING "yuma_hip 0.1.0 gfx950"
+
+namespace yk {
+
+constexpr int kTileM = 64;       // miner columns per tile: 16 lanes x float4
+constexpr int kMaxTiles = 1 << 20;
+
+// ---------------------------------------------------------------------------
+// torch-CPU-faithful scalar helpers
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float qnan() { return __builtin_nanf(""); }
+
+// torch.minimum / torch.min(a, b) / clamp(max=b): NaN in -> NaN out.
+__device__ __forceinline__ float tmin(float a, float b) {
+  if (a != a || b != b) return qnan();
+  return b < a ? b : a;
+}
+// torch.maximum / clamp(min=b): NaN in -> NaN out.
+__device__ __forceinline__ float tmax(float a, float b) {
+  if (a != a || b != b) return qnan();
+  return b > a ? b : a;
+}
+// torch.nan_to_num(x, nan=nan_v): +-inf -> +-FLT_MAX.
+__device__ __forceinline__ float nan_to_num(float x, float nan_v = 0.0f) {
+  if (x != x) return nan_v;
+  if (x == INFINITY) return FLT_MAX;
+  if (x == -INFINITY) return -FLT_MAX;
+  return x;
+}
+
+// thread -> (row group g, column quad c4). A wave covers 4 row groups x 64
+// columns, so one float4 load instruction moves 4 x 256 contiguous bytes.
+struct Lay {
+  int g, c4, lane, wave;
+};
+__device__ __forceinline__ Lay lay() {
+  Lay L;
+  L.lane = threadIdx.x & 63;
+  L.wave = threadIdx.x >> 6;
+  L.g = L.wave * 4 + (L.lane >> 4);
+  L.c4 = L.lane & 15;
+  return L;
+}
+
+// Sum over the 4 lanes of a wave that share a column quad (l, l^16, l^32,
+// l^48). IEEE addition is commutative, so every lane ends with the same bits.
+__device__ __forceinline__ float sum_rowgroups(float x) {
+  x = x + __shfl_xor(x, 16, 64);
+  x = x + __shfl_xor(x, 32, 64);
+  return x;
+}
+// Sum over the 16 lanes of one row (the 64 columns of a tile row).
+__device__ __forceinline__ float sum_row16(float x) {
+  x = x + __shfl_xor(x, 1, 64);
+  x = x + __shfl_xor(x, 2, 64);
+  x = x + __shfl_xor(x, 4, 64);
+  x = x + __shfl_xor(x, 8, 64);
+  return x;
+}
+__device__ __forceinline__ float wave_sum(float x) {
+  for (int o = 1; o < 64; o <<= 1) x = x + __shfl_xor(x, o, 64);
+  return x;
+}
+__device__ __forceinline__ double wave_sum_d(double x) {
+  for (int o = 1; o < 64; o <<= 1) x = x + __shfl_xor(x, o, 64);
+  return x;
+}
+
+// Column sums of a [rows x 64] tile: v holds this thread's partial sums for
+// its 4 columns; on return every thread holds the full column sums. Order:
+// thread-sequential rows, lane butterfly, then waves 0..NW-1 in order.
+template <int NW>
+__device__ __forceinline__ void col_reduce4(float (&v)[4], float4* red /*[NW*16]*/,
+                                            const Lay& L) {
+#pragma unroll
+  for (int c = 0; c < 4; ++c) v[c] = sum_rowgroups(v[c]);
+  if (L.lane < 16) red[L.wave * 16 + L.c4] = make_float4(v[0], v[1], v[2], v[3]);
+  __syncthreads();
+  float4 a = red[L.c4];
+#pragma unroll
+  for (int w = 1; w < NW; ++w) {
+    const float4 b = red[w * 16 + L.c4];
+    a.x = a.x + b.x;
+    a.y = a.y + b.y;
+    a.z = a.z + b.z;
+    a.w = a.w + b.w;
+  }
+  v[0] = a.x;
+  v[1] = a.y;
+  v[2] = a.z;
+  v[3] = a.w;
+}
+
+template <bool VEC>
+__device__ __forceinline__ void load4(const float* __restrict__ row, int m, int M, float (&x)[4]) {
+  if (VEC) {
+    if (m < M) {
+      const float4 t = *reinterpret_cast<const float4*>(row + m);
+      x[0] = t.x;
+      x[1] = t.y;
+      x[2] = t.z;
+      x[3] = t.w;
+    } else {
+      x[0] = x[1] = x[2] = x[3] = 0.0f;
+    }
+  } else {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) x[c] = (m + c < M) ? row[m + c] : 0.0f;
+  }
+}
+template <bool VEC>
+__device__ __forceinline__ void store4(float* __restrict__ row, int m, int M, const float (&x)[4]) {
+  if (VEC) {
+    if (m < M) *reinterpret_cast<float4*>(row + m) = make_float4(x[0], x[1], x[2], x[3]);
+  } else {
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      if (m + c < M) row[m + c] = x[c];
+  }
+}
+__device__ __forceinline__ void load4_vec(const float* __restrict__ v, int m, int M, float (&x)[4]) {
+#pragma unroll
+  for (int c = 0; c < 4; ++c) x[c] = (m + c < M) ? v[m + c] : 0.0f;
+}
+
+// ---------------------------------------------------------------------------
+// Phase 1a: row sums (yumas.py:186 `W.sum(dim=1) + 1e-6`) and S / S.sum()
+// (yumas.py:189). One wave per row. Block x: (slice, 4-row block).
+// ---------------------------------------------------------------------------
+template <bool VEC>
+__global__ __launch_bounds__(256) void k_rowsum(const float* __restrict__ W,
+                                                const float* __restrict__ S, int V, int M,
+                                                long long slice0, int rowblocks,
+                                                float* __restrict__ rsd, float* __restrict__ sn) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const long long slice = slice0 + blockIdx.x / rowblocks;
+  const int rb = blockIdx.x % rowblocks;
+  const int row = rb * 4 + wave;
+  if (row < V) {
+    const float* r = W + (slice * V + row) * (long long)M;
+    float acc = 0.0f;
+    if (VEC) {
+      for (int m = lane * 4; m < M; m += 256) {
+        const float4 t = *reinterpret_cast<const float4*>(r + m);
+        acc = acc + t.x;
+        acc = acc + t.y;
+        acc = acc + t.z;
+        acc = acc + t.w;
+      }
+    } else {
+      for (int m = lane; m < M; m += 64) acc = acc + r[m];
+    }
+    acc = wave_sum(acc);
+    if (lane == 0) rsd[slice * V + row] = acc + 1e-6f;
+  }
+  if (rb == 0 && wave == 0) {
+    const float* s = S + slice * V;
+    float acc = 0.0f;
+    for (int v = lane; v < V; v += 64) acc = acc + s[v];
+    acc = wave_sum(acc);
+    for (int v = lane; v < V; v += 64) sn[slice * V + v] = s[v] / acc;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Phase 1b: consensus bisection (yumas.py:195-209, YumaRust :81-95) + prerank
+// P = sum_v S W (yumas.py:192). Block = one 64-miner tile of one slice, the
+// whole validator column resident in registers (R rows per thread).
+// Per iteration: mid in double exactly as the reference, compared as fp32
+// (torch casts the python scalar), masked stake sums reduced in a fixed tree.
+// ---------------------------------------------------------------------------
+template <int NT, int R, bool VEC>
+__global__ __launch_bounds__(NT) void k_consensus(const float* __restrict__ W,
+                                                  const float* __restrict__ rsd,
+                                                  const float* __restrict__ sn,
+                                                  const yuma_params_t* __restrict__ prm, int N,
+                                                  int V, int M, long long slice0, int tiles,
+                                                  double* __restrict__ craw,
+                                                  float* __restrict__ Pout) {
+  constexpr int NW = NT / 64, G = NT / 16;
+  __shared__ float4 red[2][NW * 16];
+  const Lay L = lay();
+  const long long slice = slice0 + blockIdx.x / tiles;
+  const int tile = blockIdx.x % tiles;
+  const int n = (int)(slice % N);
+  const int m = tile * kTileM + L.c4 * 4;
+  const float* Ws = W + slice * (long long)V * M;
+
+  float wn[R][4], s[R];
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    const int row = L.g + G * i;
+    if (row < V) {
+      float x[4];
+      load4<VEC>(Ws + (long long)row * M, m, M, x);
+      const float d = rsd[slice * V + row];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) wn[i][c] = x[c] / d;
+      s[i] = sn[slice * V + row];
+    } else {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) wn[i][c] = 0.0f;
+      s[i] = 0.0f;
+    }
+  }
+
+  if (Pout != nullptr) {
+    float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int i = 0; i < R; ++i)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) acc[c] = acc[c] + s[i] * wn[i][c];
+    col_reduce4<NW>(acc, red[1], L);
+    if (L.g == 0)
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        if (m + c < M) Pout[slice * M + m + c] = acc[c];
+    __syncthreads();
+  }
+
+  const float kappa = prm[n].kappa;
+  const int iters = prm[n].bisect_iters;
+  double lo[4] = {0.0, 0.0, 0.0, 0.0}, hi[4] = {1.0, 1.0, 1.0, 1.0};
+  for (int it = 0; it < iters; ++it) {
+    double mid[4];
+    float midf[4], part[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      mid[c] = (hi[c] + lo[c]) / 2.0;
+      midf[c] = (float)mid[c];
+      part[c] = 0.0f;
+    }
+#pragma unroll
+    for (int i = 0; i < R; ++i)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) part[c] = part[c] + ((wn[i][c] > midf[c]) ? s[i] : 0.0f);
+    col_reduce4<NW>(part, red[it & 1], L);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      if (part[c] > kappa)
+        lo[c] = mid[c];
+      else
+        hi[c] = mid[c];
+    }
+  }
+  if (L.g == 0)
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      if (m + c < M) craw[slice * M + m + c] = hi[c];
+}
+
+// ---------------------------------------------------------------------------
+// Block-wide reductions with a fixed order (thread-sequential, wave butterfly,
+// waves in order).
+// ---------------------------------------------------------------------------
+template <int NT>
+__device__ float block_sum(float x, float* red) {
+  constexpr int NW = NT / 64;
+  x = wave_sum(x);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = x;
+  __syncthreads();
+  float t = red[0];
+  for (int w = 1; w < NW; ++w) t = t + red[w];
+  return t;
+}
+template <int NT>
+__device__ double block_sum_d(double x, double* red) {
+  constexpr int NW = NT / 64;
+  x = wave_sum_d(x);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = x;
+  __syncthreads();
+  double t = red[0];
+  for (int w = 1; w < NW; ++w) t = t + red[w];
+  return t;
+}
+
+// k-th smallest quantisation level (0-based) by a two-level 256-bin integer
+// histogram select. Integer counts are order independent, so the selection is
+// exact and deterministic. hist1 must already hold the high-byte histogram.
+template <int NT>
+__device__ int select_level(const int* __restrict__ q, int M, int k, const int* hist1,
+                            int* hist2, int* bc) {
+  if (threadIdx.x == 0) {
+    int cum = 0, b = 0;
+    for (b = 0; b < 256; ++b) {
+      if (cum + hist1[b] > k) break;
+      cum += hist1[b];
+    }
+    bc[0] = b;
+    bc[1] = k - cum;
+  }
+  for (int j = threadIdx.x; j < 256; j += NT) hist2[j] = 0;
+  __syncthreads();
+  const int b = bc[0];
+  for (int j = threadIdx.x; j < M; j += NT) {
+    const int v = min(max(q[j], 0), 65535);
+    if ((v >> 8) == b) atomicAdd(&hist2[v & 255], 1);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int kk = bc[1], cum = 0, lo = 0;
+    for (lo = 0; lo < 256; ++lo) {
+      if (cum + hist2[lo] > kk) break;
+      cum += hist2[lo];
+    }
+    bc[2] = (b << 8) | lo;
+  }
+  __syncthreads();
+  const int r = bc[2];
+  __syncthreads();
+  return r;
+}
+
+__device__ __forceinline__ float level_value(int q) { return (float)q / 65535.0f; }
+
+// torch.quantile(C, qf) on levels (Sorting.cpp: rank = q*(n-1) in fp32,
+// weight = rank - floor, lerp in the FMA form of the vectorised lerp kernel).
+template <int NT>
+__device__ float quantile_of(const int* q, int M, float qf, const int* hist1, int* hist2,
+                             int* bc) {
+  const float rank = qf * (float)(M - 1);
+  const int lo_i = (int)rank;
+  const int hi_i = (int)ceilf(rank);
+  const float w = rank - (float)lo_i;
+  const float a = level_value(select_level<NT>(q, M, lo_i, hist1, hist2, bc));
+  const float b = level_value(select_level<NT>(q, M, hi_i, hist1, hist2, bc));
+  const float diff = b - a;
+  if (fabsf(w) < 0.5f) return fmaf(w, diff, a);
+  return fmaf(-diff, 1.0f - w, b);
+}
+
+// ---------------------------------------------------------------------------
+// Phase 1c, one block per slice: C = int32(C / C.sum() * 65535) / 65535
+// (yumas.py:211; YumaRust :97 in fp64) and the liquid-alpha block
+// (yumas.py:231-253): quantiles -> a, b -> bond_alpha[m].
+// scal[slice] = {sum C, a, b, consensus_high, consensus_low, -, -, -}.
+// ---------------------------------------------------------------------------
+template <int NT>
+__global__ __launch_bounds__(NT) void k_quantise(const double* __restrict__ craw,
+                                                 const yuma_params_t* __restrict__ prm,
+                                                 int variant, int N, int M, long long slice0,
+                                                 float* __restrict__ C, int* __restrict__ qlev,
+                                                 float* __restrict__ ba,
+                                                 float* __restrict__ scal) {
+  __shared__ float redf[NT / 64];
+  __shared__ double redd[NT / 64];
+  __shared__ int hist1[256], hist2[256], bc[4];
+  const long long slice = slice0 + blockIdx.x;
+  const yuma_params_t& p = prm[slice % N];
+  const double* cr = craw + slice * M;
+  int* q = qlev + slice * M;
+  float* Cs = C + slice * M;
+
+  float sumf = 0.0f;
+  double sumd = 0.0;
+  if (variant == YUMA_VARIANT_RUST) {
+    double acc = 0.0;
+    for (int m = threadIdx.x; m < M; m += NT) acc = acc + cr[m];
+    sumd = block_sum_d<NT>(acc, redd);
+    sumf = (float)sumd;
+  } else {
+    float acc = 0.0f;
+    for (int m = threadIdx.x; m < M; m += NT) acc = acc + (float)cr[m];
+    sumf = block_sum<NT>(acc, redf);
+  }
+  for (int m = threadIdx.x; m < M; m += NT) {
+    int lev;
+    if (variant == YUMA_VARIANT_RUST) {
+      const double x = cr[m] / sumd * 65535.0;
+      lev = (int)x;
+    } else {
+      const float x = (float)cr[m] / sumf * 65535.0f;
+      lev = (int)x;
+    }
+    q[m] = lev;
+    Cs[m] = level_value(lev);
+  }
+  float a32 = qnan(), b32 = qnan(), ch = qnan(), cl = qnan();
+  if (p.liquid_mode != YUMA_LIQUID_OFF) {
+    if (p.liquid_mode == YUMA_LIQUID_CONST_AB) {
+      a32 = p.const_a;
+      b32 = p.const_b;
+      ch = (float)p.override_high;
+      cl = (float)p.override_low;
+    } else {
+      for (int j = threadIdx.x; j < 256; j += NT) hist1[j] = 0;
+      __syncthreads();
+      for (int m = threadIdx.x; m < M; m += NT) atomicAdd(&hist1[min(max(q[m], 0), 65535) >> 8], 1);
+      __syncthreads();
+      const bool H = p.override_flags & YUMA_OVR_HIGH, Lw = p.override_flags & YUMA_OVR_LOW;
+      ch = H ? (float)p.override_high : quantile_of<NT>(q, M, 0.75f, hist1, hist2, bc);
+      cl = Lw ? (float)p.override_low : quantile_of<NT>(q, M, 0.25f, hist1, hist2, bc);
+      // both overrides: the host decided the (double) equality; otherwise fp32 compare
+      const bool eq = (H && Lw) ? (p.override_flags & YUMA_OVR_FORCE_Q99) != 0 : (ch == cl);
+      if (eq) ch = quantile_of<NT>(q, M, 0.99f, hist1, hist2, bc);
+      const float d = cl - ch;
+      const float inv = 1.0f / d;
+      a32 = inv * (float)p.ln_num;
+      b32 = (float)p.ln_low + a32 * cl;
+    }
+    const float e32 = 2.71828182845904523536f;
+    for (int m = threadIdx.x; m < M; m += NT) {
+      const float x = (-a32) * Cs[m];
+      const float y = x + b32;
+      const float pw = powf(e32, y);
+      const float den = 1.0f + pw;
+      const float alpha = 1.0f / den;
+      const float clamped = tmin(tmax(alpha, p.alpha_low), p.alpha_high);
+      ba[slice * M + m] = 1.0f - clamped;
+    }
+  }
+  if (threadIdx.x == 0) {
+    float* sc = scal + slice * 8;
+    sc[0] = sumf;
+    sc[1] = a32;
+    sc[2] = b32;
+    sc[3] = ch;
+    sc[4] = cl;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Phase 1d: clip + rank (yumas.py:214-217; Yuma2 clips W_prev :328) and the
+// full-output extras (weight, clipped weight, validator-trust partials).
+// rpart[slice][tile] = sum over the tile's 64 columns of R.
+// ---------------------------------------------------------------------------
+template <int NT, int R, bool VEC>
+__global__ __launch_bounds__(NT) void k_rank(
+    const float* __restrict__ W, const float* __restrict__ rsd, const float* __restrict__ sn,
+    const float* __restrict__ C, const float* __restrict__ Wprev_init, int yuma2, int N, int V,
+    int M, long long slice0, int tiles, float* __restrict__ Rout, float* __restrict__ rpart,
+    float* __restrict__ Wn_out, float* __restrict__ Wc_out, float* __restrict__ tvc,
+    float* __restrict__ tvn) {
+  constexpr int NW = NT / 64, G = NT / 16;
+  __shared__ float4 red[NW * 16];
+  const Lay L = lay();
+  const long long slice = slice0 + blockIdx.x / tiles;
+  const int tile = blockIdx.x % tiles;
+  const int n = (int)(slice % N);
+  const long long t = slice / N;
+  const int m = tile * kTileM + L.c4 * 4;
+  const long long VM = (long long)V * M;
+  const float* Ws = W + slice * VM;
+  float Cc[4];
+  load4_vec(C + slice * M, m, M, Cc);
+
+  float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    const int row = L.g + G * i;
+    if (row >= V) continue;
+    float x[4], wn[4], src[4], wc[4];
+    load4<VEC>(Ws + (long long)row * M, m, M, x);
+    const float d = rsd[slice * V + row];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) wn[c] = x[c] / d;
+    if (yuma2) {
+      if (t == 0) {
+        if (Wprev_init != nullptr) {
+          load4<VEC>(Wprev_init + n * VM + (long long)row * M, m, M, src);
+        } else {
+#pragma unroll
+          for (int c = 0; c < 4; ++c) src[c] = wn[c];
+        }
+      } else {
+        float xp[4];
+        load4<VEC>(W + (slice - N) * VM + (long long)row * M, m, M, xp);
+        const float dp = rsd[(slice - N) * V + row];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) src[c] = xp[c] / dp;
+      }
+    } else {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) src[c] = wn[c];
+    }
+    const float s = sn[slice * V + row];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      wc[c] = tmin(src[c], Cc[c]);
+      acc[c] = acc[c] + s * wc[c];
+    }
+    if (Wn_out != nullptr) store4<VEC>(Wn_out + slice * VM + (long long)row * M, m, M, wn);
+    if (Wc_out != nullptr) store4<VEC>(Wc_out + slice * VM + (long long)row * M, m, M, wc);
+    if (tvc != nullptr) {
+      float a = 0.0f, b = 0.0f;
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        if (m + c < M) {
+          a = a + wc[c];
+          b = b + wn[c];
+        }
+      a = sum_row16(a);
+      b = sum_row16(b);
+      if (L.c4 == 0) {
+        tvc[(slice * tiles + tile) * V + row] = a;
+        tvn[(slice * tiles + tile) * V + row] = b;
+      }
+    }
+  }
+  col_reduce4<NW>(acc, red, L);
+  if (L.g == 0)
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      if (m + c < M) Rout[slice * M + m + c] = acc[c];
+  // tile sum of R in a fixed order: quad sums, lane butterfly over 16 quads
+  float ts = 0.0f;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) ts = ts + acc[c];
+  ts = sum_row16(ts);
+  if (threadIdx.x == 0) rpart[slice * tiles + tile] = ts;
+}
+
+// ---------------------------------------------------------------------------
+// Phase 1e, one block per slice: I = nan_to_num(R / R.sum(), 0) and the
+// server trust T = nan_to_num(R / P) (yumas.py:220-223).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_incentive(const float* __restrict__ Rin,
+                                                   const float* __restrict__ rpart,
+                                                   const float* __restrict__ Pin, int M,
+                                                   long long slice0, int tiles,
+                                                   float* __restrict__ I, float* __restrict__ T,
+                                                   float* __restrict__ scal) {
+  __shared__ float tot;
+  const long long slice = slice0 + blockIdx.x;
+  if (threadIdx.x == 0) {
+    float s = 0.0f;
+    for (int k = 0; k < tiles; ++k) s = s + rpart[slice * tiles + k];
+    tot = s;
+    scal[slice * 8 + 5] = s;
+  }
+  __syncthreads();
+  const float sr = tot;
+  for (int m = threadIdx.x; m < M; m += 256) {
+    const float r = Rin[slice * M + m];
+    I[slice * M + m] = nan_to_num(r / sr, 0.0f);
+    if (T != nullptr) T[slice * M + m] = nan_to_num(r / Pin[slice * M + m], 0.0f);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Phase 2: bond recurrence over the epochs [t0, t1) of a chunk, one block per
+// (scenario, row block, 64-miner tile); the bond tile stays in registers.
+//   VARIANT 3 (yumas.py:452-472) and 4 (:570-586) are element-wise, so a block
+//   owns R*G rows of the tile. VARIANT 0/1/2 normalise bond columns over all
+//   validators (yumas.py:113-116,147-149; :228; :342), so a block owns the
+//   whole column (single row block).
+// dpart[slice][tile][v] = sum over the tile's columns of B_state * I.
+// ---------------------------------------------------------------------------
+struct BondArgs {
+  const float* W;
+  const float* rsd;
+  const float* sn;
+  const float* C;
+  const float* I;
+  const float* ba;  // liquid bond_alpha [slice][M] (read for liquid scenarios)
+  const yuma_params_t* prm;
+  const float* B_init;
+  const float* Wprev_init;
+  float* Bstate;  // [N][V][M]
+  float* B_hist;
+  float* Wb_out;
+  float* Binst_out;
+  float* dpart;
+  int N, V, M, tiles, rowblocks, t0, t1;
+};
+
+template <int VARIANT, int NT, int R, bool VEC>
+__global__ __launch_bounds__(NT) void k_bonds(BondArgs A) {
+  constexpr int NW = NT / 64, G = NT / 16;
+  constexpr bool COLNORM = (VARIANT == YUMA_VARIANT_RUST || VARIANT == YUMA_VARIANT_YUMA1 ||
+                            VARIANT == YUMA_VARIANT_YUMA2);
+  __shared__ float4 red[2][NW * 16];
+  const Lay L = lay();
+  const int tile = blockIdx.x % A.tiles;
+  const int rb = (blockIdx.x / A.tiles) % A.rowblocks;
+  const int n = blockIdx.x / (A.tiles * A.rowblocks);
+  const int N = A.N, V = A.V, M = A.M;
+  const long long VM = (long long)V * M;
+  const int m = tile * kTileM + L.c4 * 4;
+  const yuma_params_t& p = A.prm[n];
+  const int row0 = rb * G * R + L.g;
+
+  float B[R][4];
+  float Wp[R][4];  // Yuma2: previous epoch's normalised W
+  bool has_old;
+  if (A.t0 == 0) {
+    has_old = A.B_init != nullptr;
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const int row = row0 + G * i;
+      if (has_old && row < V)
+        load4<VEC>(A.B_init + n * VM + (long long)row * M, m, M, B[i]);
+      else
+#pragma unroll
+        for (int c = 0; c < 4; ++c) B[i][c] = 0.0f;
+    }
+  } else {
+    has_old = true;
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const int row = row0 + G * i;
+      if (row < V)
+        load4<VEC>(A.Bstate + n * VM + (long long)row * M, m, M, B[i]);
+      else
+#pragma unroll
+        for (int c = 0; c < 4; ++c) B[i][c] = 0.0f;
+    }
+  }
+  bool have_wp = false;
+  if (VARIANT == YUMA_VARIANT_YUMA2) {
+    if (A.t0 == 0) {
+      if (A.Wprev_init != nullptr) {
+        have_wp = true;
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+          const int row = row0 + G * i;
+          if (row < V)
+            load4<VEC>(A.Wprev_init + n * VM + (long long)row * M, m, M, Wp[i]);
+          else
+#pragma unroll
+            for (int c = 0; c < 4; ++c) Wp[i][c] = 0.0f;
+        }
+      }
+    } else {
+      have_wp = true;
+      const long long ps = (long long)(A.t0 - 1) * N + n;
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        const int row = row0 + G * i;
+        if (row < V) {
+          float x[4];
+          load4<VEC>(A.W + ps * VM + (long long)row * M, m, M, x);
+          const float d = A.rsd[ps * V + row];
+#pragma unroll
+          for (int c = 0; c < 4; ++c) Wp[i][c] = x[c] / d;
+        } else {
+#pragma unroll
+          for (int c = 0; c < 4; ++c) Wp[i][c] = 0.0f;
+        }
+      }
+    }
+  }
+
+  for (int t = A.t0; t < A.t1; ++t) {
+    const long long slice = (long long)t * N + n;
+    // bond resets of run_simulation (simulation_utils.py:62-88), applied to
+    // the state before this epoch's update
+    if ((VARIANT == YUMA_VARIANT_YUMA3 || VARIANT == YUMA_VARIANT_YUMA4) && has_old &&
+        p.reset_mode != YUMA_RESET_NONE && t == p.reset_epoch && p.reset_index >= 0 &&
+        p.reset_index < M) {
+      bool fire = p.reset_mode == YUMA_RESET_ALWAYS;
+      if (p.reset_mode == YUMA_RESET_IF_ZERO_CONSENSUS && t >= 1)
+        fire = A.C[(slice - N) * M + p.reset_index] == 0.0f;
+      const int c = p.reset_index - m;
+      if (fire && c >= 0 && c < 4)
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+#pragma unroll
+          for (int cc = 0; cc < 4; ++cc)
+            if (cc == c) B[i][cc] = 0.0f;
+        }
+    }
+    float Ic[4], Cc[4], bac[4], omba[4];
+    load4_vec(A.I + slice * M, m, M, Ic);
+    if (COLNORM) load4_vec(A.C + slice * M, m, M, Cc);
+    if (p.liquid_mode != YUMA_LIQUID_OFF) {
+      load4_vec(A.ba + slice * M, m, M, bac);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) omba[c] = 1.0f - bac[c];
+    } else {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        bac[c] = p.bond_alpha;
+        omba[c] = p.one_minus_bond_alpha;
+      }
+    }
+
+    float wn[R][4], s[R];
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const int row = row0 + G * i;
+      if (row < V) {
+        float x[4];
+        load4<VEC>(A.W + slice * VM + (long long)row * M, m, M, x);
+        const float d = A.rsd[slice * V + row];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) wn[i][c] = x[c] / d;
+        s[i] = A.sn[slice * V + row];
+      } else {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) wn[i][c] = 0.0f;
+        s[i] = 0.0f;
+      }
+    }
+
+    if (VARIANT == YUMA_VARIANT_YUMA3) {
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        const float cap = s[i] * p.maxint;
+        const float ca = p.capacity_alpha * cap;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const float rem = tmax(cap - B[i][c], 0.0f);
+          const float pc = tmin(ca, rem);
+          const float purchase = pc * wn[i][c];
+          const float nb = p.decay_keep * B[i][c] + purchase;
+          B[i][c] = tmin(nb, cap);
+        }
+      }
+    } else if (VARIANT == YUMA_VARIANT_YUMA4) {
+#pragma unroll
+      for (int i = 0; i < R; ++i)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const float bd = B[i][c] * omba[c];
+          const float rem = tmax(1.0f - bd, 0.0f);
+          const float pi = bac[c] * wn[i][c];
+          const float nb = bd + tmin(pi, rem);
+          B[i][c] = tmin(nb, 1.0f);
+        }
+    } else {
+      // column-normalised variants
+      float num[R][4];
+      float colsum[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        const int row = row0 + G * i;
+        float src[4], wc[4], wb[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          src[c] = (VARIANT == YUMA_VARIANT_YUMA2 && have_wp) ? Wp[i][c] : wn[i][c];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) wc[c] = tmin(src[c], Cc[c]);
+        if (VARIANT == YUMA_VARIANT_RUST) {
+#pragma unroll
+          for (int c = 0; c < 4; ++c) num[i][c] = s[i] * wc[c];
+        } else {
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            wb[c] = p.one_minus_bond_penalty * src[c] + p.bond_penalty * wc[c];
+            num[i][c] = s[i] * wb[c];
+          }
+          if (A.Wb_out != nullptr && row < V)
+            store4<VEC>(A.Wb_out + slice * VM + (long long)row * M, m, M, wb);
+        }
+#pragma unroll
+        for (int c = 0; c < 4; ++c) colsum[c] = colsum[c] + num[i][c];
+      }
+      col_reduce4<NW>(colsum, red[0], L);
+      float den[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        den[c] = (VARIANT == YUMA_VARIANT_RUST) ? colsum[c] + 1e-6f : colsum[c];
+      float ema_sum[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        const int row = row0 + G * i;
+        float binst[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const float b = num[i][c] / den[c];
+          binst[c] = (VARIANT == YUMA_VARIANT_RUST) ? nan_to_num(b, 0.0f) : nan_to_num(b, 0.0f);
+        }
+        if (A.Binst_out != nullptr && row < V)
+          store4<VEC>(A.Binst_out + slice * VM + (long long)row * M, m, M, binst);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          float e = binst[c];
+          if (has_old) e = bac[c] * binst[c] + omba[c] * B[i][c];
+          if (row >= V) e = 0.0f;
+          B[i][c] = e;
+          ema_sum[c] = ema_sum[c] + e;
+        }
+      }
+      if (VARIANT == YUMA_VARIANT_RUST) {
+        col_reduce4<NW>(ema_sum, red[1], L);
+#pragma unroll
+        for (int i = 0; i < R; ++i)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) B[i][c] = nan_to_num(B[i][c] / (ema_sum[c] + 1e-6f), 0.0f);
+      }
+      if (VARIANT == YUMA_VARIANT_YUMA2) {
+#pragma unroll
+        for (int i = 0; i < R; ++i)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) Wp[i][c] = wn[i][c];
+        have_wp = true;
+      }
+    }
+    has_old = true;
+
+    // state history + dividend partials
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const int row = row0 + G * i;
+      if (A.B_hist != nullptr && row < V)
+        store4<VEC>(A.B_hist + slice * VM + (long long)row * M, m, M, B[i]);
+      float d = 0.0f;
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        if (m + c < M) d = d + B[i][c] * Ic[c];
+      d = sum_row16(d);
+      if (L.c4 == 0 && row < V) A.dpart[(slice * A.tiles + tile) * V + row] = d;
+    }
+    if (COLNORM) __syncthreads();  // red[] reuse across epochs
+  }
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    const int row = row0 + G * i;
+    if (row < V) store4<VEC>(A.Bstate + n * VM + (long long)row * M, m, M, B[i]);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Finalize, one block per slice: D = sum over tiles of the partials (Yuma4:
+// D = S * that, yumas.py:590), D_normalized = D / (D.sum() + 1e-6), and
+// validator trust T_v = sum Wc / sum W (yumas.py:224).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_finalize(const float* __restrict__ dpart,
+                                                  const float* __restrict__ sn, int variant,
+                                                  int V, long long slice0, int tiles,
+                                                  const float* __restrict__ tvc,
+                                                  const float* __restrict__ tvn,
+                                                  float* __restrict__ Dn, float* __restrict__ D,
+                                                  float* __restrict__ Tv) {
+  __shared__ float red[4];
+  const long long slice = slice0 + blockIdx.x;
+  float local = 0.0f;
+  // V <= 1024: each thread owns v = tid + 256 j
+  float dv[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int v = threadIdx.x + 256 * j;
+    float d = 0.0f;
+    if (v < V) {
+      for (int k = 0; k < tiles; ++k) d = d + dpart[(slice * tiles + k) * V + v];
+      if (variant == YUMA_VARIANT_YUMA4) d = sn[slice * V + v] * d;
+      local = local + d;
+    }
+    dv[j] = d;
+  }
+  const float tot = block_sum<256>(local, red);
+  const float den = tot + 1e-6f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int v = threadIdx.x + 256 * j;
+    if (v < V) {
+      if (Dn != nullptr) Dn[slice * V + v] = dv[j] / den;
+      if (D != nullptr) D[slice * V + v] = dv[j];
+      if (Tv != nullptr) {
+        float a = 0.0f, b = 0.0f;
+        for (int k = 0; k < tiles; ++k) {
+          a = a + tvc[(slice * tiles + k) * V + v];
+          b = b + tvn[(slice * tiles + k) * V + v];
+        }
+        Tv[slice * V + v] = a / b;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Synthetic weights, integer-only so numpy and HIP agree bit for
+// bit: see yuma_simulation/_internal/synth.py for the reference definition.
+// ---------------------------------------------------------------------------
+__host__ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+  uint64_t z = x + 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+__host__ __device__ __forceinline__ uint64_t hash3(uint64_t seed, uint64_t a, uint64_t b,
+                                                   uint64_t c) {
+  return splitmix64(splitmix64(splitmix64(seed ^ a) ^ b) ^ c);
+}
+constexpr uint64_t kTagWeight = 1ull << 63, kTagZero = 1ull << 62, kTagQuality = 1ull << 61;
+
+__global__ void k_synth(uint64_t seed, int E, int N, int V, int M, int t0, float* __restrict__ W) {
+  const long long total = (long long)E * N * V * M;
+  const uint64_t wmax = (uint64_t)((16777215ull) / (uint64_t)M);
+  for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (long long)gridDim.x * blockDim.x) {
+    const int m = (int)(idx % M);
+    const int v = (int)((idx / M) % V);
+    const long long sl = idx / ((long long)V * M);
+    const int n = (int)(sl % N);
+    const int t = (int)(sl / N) + t0;
+    const uint64_t sd = seed + 0x1000003ull * (uint64_t)n;
+    const uint64_t qa = hash3(sd, kTagQuality, 0, (uint64_t)m) >> 40;
+    const uint64_t Q = (1ull << 22) + ((3ull * qa) >> 2);
+    const uint64_t ua = hash3(sd, kTagWeight | (uint64_t)t, (uint64_t)v, (uint64_t)m) >> 40;
+    const uint64_t F = (3ull * (1ull << 24) + 4ull * ua) / 5ull;
+    uint64_t w = (Q * F) >> 24;
+    if (w > (1ull << 24)) w = 1ull << 24;
+    uint64_t val = (w * wmax) >> 24;
+    const uint64_t z = hash3(sd, kTagZero | (uint64_t)t, (uint64_t)v, (uint64_t)m) >> 40;
+    if (z < 1677722ull) val = 0;
+    W[idx] = (float)val;
+  }
+}
+
+}  // namespace yk
+
+// ===========================================================================
+// Host side: workspace carving, dispatch, C-ABI
+// ===========================================================================
+namespace {
+
+thread_local char g_err[512] = "";
+
+int fail(int code, const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+  return code;
+}
+
+size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
+
+struct Workspace {
+  float* rsd;
+  float* sn;
+  double* craw;
+  int* qlev;
+  float* C;
+  float* R;
+  float* I;
+  float* ba;
+  float* rpart;
+  float* dpart;
+  float* scal;
+  float* tvc;
+  float* tvn;
+  float* Bstate;
+  size_t bytes;
+};
+
+Workspace carve(char* base, int variant, int N, int E, int V, int M, int full) {
+  (void)variant;
+  Workspace w{};
+  const size_t S = (size_t)E * N;
+  const size_t tiles = (size_t)(M + yk::kTileM - 1) / yk::kTileM;
+  size_t off = 0;
+  auto take = [&](size_t bytes) -> char* {
+    char* p = base ? base + off : nullptr;
+    off += align256(bytes);
+    return p;
+  };
+  w.rsd = (float*)take(S * V * 4);
+  w.sn = (float*)take(S * V * 4);
+  w.craw = (double*)take(S * M * 8);
+  w.qlev = (int*)take(S * M * 4);
+  w.C = (float*)take(S * M * 4);
+  w.R = (float*)take(S * M * 4);
+  w.I = (float*)take(S * M * 4);
+  w.ba = (float*)take(S * M * 4);
+  w.rpart = (float*)take(S * tiles * 4);
+  w.dpart = (float*)take(S * tiles * V * 4);
+  w.scal = (float*)take(S * 8 * 4);
+  w.tvc = full ? (float*)take(S * tiles * V * 4) : nullptr;
+  w.tvn = full ? (float*)take(S * tiles * V * 4) : nullptr;
+  w.Bstate = (float*)take((size_t)N * V * M * 4);
+  w.bytes = off;
+  return w;
+}
+
+bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+// Row-configuration of the column-resident kernels: NT threads, R rows each.
+enum RowCfg { RC_256_1, RC_256_4, RC_256_16, RC_1024_16 };
+RowCfg row_cfg(int V) {
+  if (V <= 16) return RC_256_1;
+  if (V <= 64) return RC_256_4;
+  if (V <= 256) return RC_256_16;
+  return RC_1024_16;
+}
+
+#define YK_LAUNCH(kernel, grid, block, stream, ...) \
+  hipLaunchKernelGGL(kernel, dim3(grid), dim3(block), 0, (hipStream_t)(stream), __VA_ARGS__)
+
+template <bool VEC>
+void launch_consensus(RowCfg rc, long long nblocks, hipStream_t st, const float* W,
+                      const float* rsd, const float* sn, const yuma_params_t* prm, int N, int V,
+                      int M, long long slice0, int tiles, double* craw, float* P) {
+  switch (rc) {
+    case RC_256_1:
+      YK_LAUNCH((yk::k_consensus<256, 1, VEC>), nblocks, 256, st, W, rsd, sn, prm, N, V, M,
+                slice0, tiles, craw, P);
+      break;
+    case RC_256_4:
+      YK_LAUNCH((yk::k_consensus<256, 4, VEC>), nblocks, 256, st, W, rsd, sn, prm, N, V, M,
+                slice0, tiles, craw, P);
+      break;
+    case RC_256_16:
+      YK_LAUNCH((yk::k_consensus<256, 16, VEC>), nblocks, 256, st, W, rsd, sn, prm, N, V, M,
+                slice0, tiles, craw, P);
+      break;
+    case RC_1024_16:
+      YK_LAUNCH((yk::k_consensus<1024, 16, VEC>), nblocks, 1024, st, W, rsd, sn, prm, N, V, M,
+                slice0, tiles, craw, P);
+      break;
+  }
+}
+
+template <bool VEC>
+void launch_rank(RowCfg rc, long long nblocks, hipStream_t st, const float* W, const float* rsd,
+                 const float* sn, const float* C, const float* Wprev_init, int yuma2, int N,
+                 int V, int M, long long slice0, int tiles, float* R, float* rpart, float* Wn,
+                 float* Wc, float* tvc, float* tvn) {
+  switch (rc) {
+    case RC_256_1:
+      YK_LAUNCH((yk::k_rank<256, 1, VEC>), nblocks, 256, st, W, rsd, sn, C, Wprev_init, yuma2,
+                N, V, M, slice0, tiles, R, rpart, Wn, Wc, tvc, tvn);
+      break;
+    case RC_256_4:
+      YK_LAUNCH((yk::k_rank<256, 4, VEC>), nblocks, 256, st, W, rsd, sn, C, Wprev_init, yuma2,
+                N, V, M, slice0, tiles, R, rpart, Wn, Wc, tvc, tvn);
+      break;
+    case RC_256_16:
+      YK_LAUNCH((yk::k_rank<256, 16, VEC>), nblocks, 256, st, W, rsd, sn, C, Wprev_init, yuma2,
+                N, V, M, slice0, tiles, R, rpart, Wn, Wc, tvc, tvn);
+      break;
+    case RC_1024_16:
+      YK_LAUNCH((yk::k_rank<1024, 16, VEC>), nblocks, 1024, st, W, rsd, sn, C, Wprev_init,
+                yuma2, N, V, M, slice0, tiles, R, rpart, Wn, Wc, tvc, tvn);
+      break;
+  }
+}
+
+template <int VARIANT, bool VEC>
+void launch_bonds_colnorm(RowCfg rc, long long nblocks, hipStream_t st, const yk::BondArgs& A) {
+  switch (rc) {
+    case RC_256_1:
+      YK_LAUNCH((yk::k_bonds<VARIANT, 256, 1, VEC>), nblocks, 256, st, A);
+      break;
+    case RC_256_4:
+      YK_LAUNCH((yk::k_bonds<VARIANT, 256, 4, VEC>), nblocks, 256, st, A);
+      break;
+    case RC_256_16:
+      YK_LAUNCH((yk::k_bonds<VARIANT, 256, 16, VEC>), nblocks, 256, st, A);
+      break;
+    case RC_1024_16:
+      YK_LAUNCH((yk::k_bonds<VARIANT, 1024, 16, VEC>), nblocks, 1024, st, A);
+      break;
+  }
+}
+
+// Element-wise variants: 256 threads, R rows per thread (R*16 rows per block).
+template <int VARIANT, bool VEC>
+void launch_bonds_elem(int R, long long nblocks, hipStream_t st, const yk::BondArgs& A) {
+  if (R == 1)
+    YK_LAUNCH((yk::k_bonds<VARIANT, 256, 1, VEC>), nblocks, 256, st, A);
+  else
+    YK_LAUNCH((yk::k_bonds<VARIANT, 256, 4, VEC>), nblocks, 256, st, A);
+}
+
+template <bool VEC>
+void launch_bonds(int variant, RowCfg rc, int elemR, long long nblocks, hipStream_t st,
+                  const yk::BondArgs& A) {
+  switch (variant) {
+    case YUMA_VARIANT_RUST:
+      launch_bonds_colnorm<YUMA_VARIANT_RUST, VEC>(rc, nblocks, st, A);
+      break;
+    case YUMA_VARIANT_YUMA1:
+      launch_bonds_colnorm<YUMA_VARIANT_YUMA1, VEC>(rc, nblocks, st, A);
+      break;
+    case YUMA_VARIANT_YUMA2:
+      launch_bonds_colnorm<YUMA_VARIANT_YUMA2, VEC>(rc, nblocks, st, A);
+      break;
+    case YUMA_VARIANT_YUMA3:
+      launch_bonds_elem<YUMA_VARIANT_YUMA3, VEC>(elemR, nblocks, st, A);
+      break;
+    default:
+      launch_bonds_elem<YUMA_VARIANT_YUMA4, VEC>(elemR, nblocks, st, A);
+      break;
+  }
+}
+
+// Optional per-phase timing (bench / roofline): HIP events recorded on the
+// launch stream between phases; elapsed times summed over chunks.
+struct PhaseTimer {
+  float* ms;  // [YUMA_NUM_PHASES] accumulated milliseconds, or nullptr
+  hipStream_t st;
+  hipEvent_t ev[YUMA_NUM_PHASES + 1][64];
+  int nchunks;
+  int ok;
+  void begin(int chunk_idx, int phase) {
+    if (ms && ok && chunk_idx < 64) (void)hipEventRecord(ev[phase][chunk_idx], st);
+  }
+};
+
+int run_impl(int variant, const yuma_params_t* prm, int N, int E, int V, int M, const float* W,
+             const float* S, const float* B_init, const float* Wprev_init,
+             const yuma_outputs_t* out, void* workspace, size_t ws_bytes, int chunk,
+             void* stream, float* phase_ms = nullptr) {
+  if (variant < 0 || variant > 4) return fail(YUMA_EINVAL, "unknown variant %d", variant);
+  if (N < 1 || E < 1 || V < 1 || M < 1)
+    return fail(YUMA_EINVAL, "sizes must be positive (N=%d E=%d V=%d M=%d)", N, E, V, M);
+  if (V > YUMA_MAX_VALIDATORS)
+    return fail(YUMA_EUNSUPPORTED, "V=%d exceeds YUMA_MAX_VALIDATORS=%d", V,
+                YUMA_MAX_VALIDATORS);
+  if ((M + yk::kTileM - 1) / yk::kTileM > yk::kMaxTiles) return fail(YUMA_EINVAL, "M too large");
+  if (!prm || !W || !S || !out || !workspace)
+    return fail(YUMA_EINVAL, "null params/W/S/outputs/workspace");
+  const int full = out->Tv != nullptr;
+  Workspace ws = carve((char*)workspace, variant, N, E, V, M, full);
+  if (ws.bytes > ws_bytes)
+    return fail(YUMA_EWORKSPACE, "workspace %zu < required %zu bytes (full_outputs=%d)",
+                ws_bytes, ws.bytes, full);
+  hipStream_t st = (hipStream_t)stream;
+  const int tiles = (M + yk::kTileM - 1) / yk::kTileM;
+  const RowCfg rc = row_cfg(V);
+  const long long slice_elems = (long long)V * M;
+
+  bool vec = (M % 4) == 0 && aligned16(W);
+  const float* mats[] = {B_init, Wprev_init, out->Wn, out->Wc, out->Wb, out->B_inst,
+                         out->B_hist, out->B_final};
+  for (const float* p : mats)
+    if (p != nullptr && !aligned16(p)) vec = false;
+
+  float* C = out->C ? out->C : ws.C;
+  float* I = out->I ? out->I : ws.I;
+  float* Bstate = out->B_final ? out->B_final : ws.Bstate;
+  // liquid bond_alpha lives in the caller's buffer when requested; scenarios
+  // with liquid_mode OFF neither write nor read it
+  float* ba_buf = out->bond_alpha ? out->bond_alpha : ws.ba;
+
+  if (chunk <= 0) {
+    const long long target = 128ll << 20;  // keep a chunk's W inside the 256 MB MALL
+    long long c = target / ((long long)N * slice_elems * 4);
+    chunk = (int)(c < 1 ? 1 : (c > E ? E : c));
+  }
+
+  const int elemR = V <= 16 ? 1 : 4;
+  const int colnorm = variant <= YUMA_VARIANT_YUMA2;
+  const int rowblocks = colnorm ? 1 : (V + 16 * elemR - 1) / (16 * elemR);
+
+  PhaseTimer tm{};
+  tm.ms = phase_ms;
+  tm.st = st;
+  tm.nchunks = (E + chunk - 1) / chunk;
+  tm.ok = 1;
+  if (phase_ms != nullptr) {
+    if (tm.nchunks > 64) return fail(YUMA_EINVAL, "profiled runs support at most 64 chunks");
+    for (int ph = 0; ph <= YUMA_NUM_PHASES; ++ph)
+      for (int c = 0; c < tm.nchunks; ++c)
+        if (hipEventCreate(&tm.ev[ph][c]) != hipSuccess) tm.ok = 0;
+    if (!tm.ok) return fail(YUMA_EHIP, "hipEventCreate failed");
+  }
+
+  for (int c0 = 0, ci = 0; c0 < E; c0 += chunk, ++ci) {
+    const int c1 = c0 + chunk < E ? c0 + chunk : E;
+    const long long s0 = (long long)c0 * N;
+    const long long ns = (long long)(c1 - c0) * N;
+    const int rowblocks4 = (V + 3) / 4;
+    tm.begin(ci, 0);
+    if (vec)
+      YK_LAUNCH(yk::k_rowsum<true>, ns * rowblocks4, 256, st, W, S, V, M, s0, rowblocks4,
+                ws.rsd, ws.sn);
+    else
+      YK_LAUNCH(yk::k_rowsum<false>, ns * rowblocks4, 256, st, W, S, V, M, s0, rowblocks4,
+                ws.rsd, ws.sn);
+    tm.begin(ci, 1);
+    if (vec)
+      launch_consensus<true>(rc, ns * tiles, st, W, ws.rsd, ws.sn, prm, N, V, M, s0, tiles,
+                             ws.craw, out->P);
+    else
+      launch_consensus<false>(rc, ns * tiles, st, W, ws.rsd, ws.sn, prm, N, V, M, s0, tiles,
+                              ws.craw, out->P);
+    tm.begin(ci, 2);
+    YK_LAUNCH(yk::k_quantise<256>, ns, 256, st, ws.craw, prm, variant, N, M, s0, C, ws.qlev,
+              ba_buf, ws.scal);
+    tm.begin(ci, 3);
+    if (vec)
+      launch_rank<true>(rc, ns * tiles, st, W, ws.rsd, ws.sn, C, Wprev_init,
+                        variant == YUMA_VARIANT_YUMA2, N, V, M, s0, tiles, out->R ? out->R : ws.R,
+                        ws.rpart, out->Wn, out->Wc, ws.tvc, ws.tvn);
+    else
+      launch_rank<false>(rc, ns * tiles, st, W, ws.rsd, ws.sn, C, Wprev_init,
+                         variant == YUMA_VARIANT_YUMA2, N, V, M, s0, tiles,
+                         out->R ? out->R : ws.R, ws.rpart, out->Wn, out->Wc, ws.tvc, ws.tvn);
+    tm.begin(ci, 4);
+    YK_LAUNCH(yk::k_incentive, ns, 256, st, out->R ? out->R : ws.R, ws.rpart, out->P, M, s0,
+              tiles, I, out->P ? out->T : nullptr, ws.scal);
+
+    yk::BondArgs A{};
+    A.W = W;
+    A.rsd = ws.rsd;
+    A.sn = ws.sn;
+    A.C = C;
+    A.I = I;
+    A.ba = ba_buf;
+    A.prm = prm;
+    A.B_init = B_init;
+    A.Wprev_init = Wprev_init;
+    A.Bstate = Bstate;
+    A.B_hist = out->B_hist;
+    A.Wb_out = out->Wb;
+    A.Binst_out = out->B_inst;
+    A.dpart = ws.dpart;
+    A.N = N;
+    A.V = V;
+    A.M = M;
+    A.tiles = tiles;
+    A.rowblocks = rowblocks;
+    A.t0 = c0;
+    A.t1 = c1;
+    const long long nb = (long long)N * tiles * rowblocks;
+    tm.begin(ci, 5);
+    if (vec)
+      launch_bonds<true>(variant, rc, elemR, nb, st, A);
+    else
+      launch_bonds<false>(variant, rc, elemR, nb, st, A);
+    tm.begin(ci, 6);
+    YK_LAUNCH(yk::k_finalize, ns, 256, st, ws.dpart, ws.sn, variant, V, s0, tiles, ws.tvc,
+              ws.tvn, out->Dn, out->D, out->Tv);
+    if (out->Sn != nullptr)
+      (void)hipMemcpyAsync(out->Sn + s0 * V, ws.sn + s0 * V, (size_t)ns * V * 4,
+                           hipMemcpyDeviceToDevice, st);
+    if (out->alpha_ab != nullptr)
+      (void)hipMemcpy2DAsync(out->alpha_ab + s0 * 2, 2 * sizeof(float), ws.scal + s0 * 8 + 1,
+                             8 * sizeof(float), 2 * sizeof(float), (size_t)ns,
+                             hipMemcpyDeviceToDevice, st);
+    tm.begin(ci, YUMA_NUM_PHASES);
+  }
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(YUMA_EHIP, "HIP launch failed: %s", hipGetErrorString(e));
+  if (phase_ms != nullptr) {
+    // bench-only path: waits for the stream, then sums per-phase elapsed times
+    for (int ph = 0; ph < YUMA_NUM_PHASES; ++ph) phase_ms[ph] = 0.0f;
+    if (hipEventSynchronize(tm.ev[YUMA_NUM_PHASES][tm.nchunks - 1]) != hipSuccess)
+      return fail(YUMA_EHIP, "hipEventSynchronize failed");
+    for (int c = 0; c < tm.nchunks; ++c)
+      for (int ph = 0; ph < YUMA_NUM_PHASES; ++ph) {
+        float t = 0.0f;
+        (void)hipEventElapsedTime(&t, tm.ev[ph][c], tm.ev[ph + 1][c]);
+        phase_ms[ph] += t;
+      }
+    for (int ph = 0; ph <= YUMA_NUM_PHASES; ++ph)
+      for (int c = 0; c < tm.nchunks; ++c) (void)hipEventDestroy(tm.ev[ph][c]);
+  }
+  return YUMA_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t yuma_workspace_bytes(int variant, int N, int E, int V, int M, int full_outputs) {
+  if (N < 1 || E < 1 || V < 1 || M < 1) return 0;
+  return carve(nullptr, variant, N, E, V, M, full_outputs).bytes;
+}
+
+int yuma_run(int variant, const yuma_params_t* params_dev, int N, int E, int V, int M,
+             const float* W, const float* S, const float* B_init, const float* Wprev_init,
+             const yuma_outputs_t* out, void* workspace, size_t workspace_bytes,
+             int chunk_epochs, void* stream) {
+  return run_impl(variant, params_dev, N, E, V, M, W, S, B_init, Wprev_init, out, workspace,
+                  workspace_bytes, chunk_epochs, stream);
+}
+
+int yuma_run_profiled(int variant, const yuma_params_t* params_dev, int N, int E, int V, int M,
+                      const float* W, const float* S, const float* B_init,
+                      const float* Wprev_init, const yuma_outputs_t* out, void* workspace,
+                      size_t workspace_bytes, int chunk_epochs, void* stream, float* phase_ms) {
+  if (phase_ms == nullptr) return fail(YUMA_EINVAL, "phase_ms is required");
+  return run_impl(variant, params_dev, N, E, V, M, W, S, B_init, Wprev_init, out, workspace,
+                  workspace_bytes, chunk_epochs, stream, phase_ms);
+}
+
+int yuma_epoch(int variant, const yuma_params_t* params_dev, int N, int V, int M,
+               const float* W, const float* W_prev, const float* S, const float* B_old,
+               const yuma_outputs_t* out, void* workspace, size_t workspace_bytes,
+               void* stream) {
+  return run_impl(variant, params_dev, N, 1, V, M, W, S, B_old, W_prev, out, workspace,
+                  workspace_bytes, 1, stream);
+}
+
+int yuma_synth_weights(uint64_t seed, int E, int N, int V, int M, int t0, float* W,
+                       void* stream) {
+  if (E < 1 || N < 1 || V < 1 || M < 1 || !W) return fail(YUMA_EINVAL, "bad synth args");
+  if (M > 16777215) return fail(YUMA_EINVAL, "M too large for exact synthetic weights");
+  const long long total = (long long)E * N * V * M;
+  long long blocks = (total + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  YK_LAUNCH(yk::k_synth, blocks, 256, stream, seed, E, N, V, M, t0, W);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(YUMA_EHIP, "HIP launch failed: %s", hipGetErrorString(e));
+  return YUMA_OK;
+}
+
+const char* yuma_last_error(void) { return g_err; }
+const char* yuma_version(void) { return YUMA_VERSION_STRING; }
+
+}  // extern "C"

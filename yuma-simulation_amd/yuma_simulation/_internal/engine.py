@@ -1,0 +1,327 @@
+"""ctypes binding of libyuma_hip.so (include/yuma_hip.h) — the only compute path.
+
+The product never falls back to CPU: if the HIP library or a GPU is missing,
+every compute entry point raises ``EngineUnavailable``. Tensors are handed over
+as raw device pointers; the engine is stream-ordered on torch's current stream
+and allocates nothing (the workspace is a torch uint8 tensor).
+
+Parameter marshalling mirrors how the reference's torch ops round Python
+scalars (yumas.py:7-45 configs, used at :186-262 and copies):
+  * a Python float meeting an fp32 tensor is rounded to fp32 first;
+  * ``1 - x`` of two Python floats is computed in double, then rounded;
+  * the bisection trip count is the reference's own loop evaluated in double.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import math
+import os
+import threading
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+LIB_NAME = "libyuma_hip.so"
+_PKG_ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+LIB_PATH = os.environ.get("YUMA_HIP_LIB", os.path.join(_PKG_ROOT, "lib", LIB_NAME))
+
+VARIANT_RUST, VARIANT_YUMA1, VARIANT_YUMA2, VARIANT_YUMA3, VARIANT_YUMA4 = range(5)
+PHASES = ("rowsum", "consensus", "quantise", "rank", "incentive", "bonds", "finalize")
+RESET_NONE, RESET_ALWAYS, RESET_IF_ZERO_CONSENSUS = range(3)
+LIQUID_OFF, LIQUID_QUANTILE, LIQUID_CONST_AB = range(3)
+OVR_HIGH, OVR_LOW, OVR_FORCE_Q99 = 1, 2, 4
+
+EXPORTED_SYMBOLS = (
+    "yuma_workspace_bytes",
+    "yuma_run",
+    "yuma_run_profiled",
+    "yuma_epoch",
+    "yuma_synth_weights",
+    "yuma_last_error",
+    "yuma_version",
+)
+
+
+class EngineUnavailable(RuntimeError):
+    """The HIP engine cannot run here (library not built or no GPU)."""
+
+
+class EngineError(RuntimeError):
+    """The engine rejected a call (bad sizes, workspace, launch failure)."""
+
+
+class YumaParamsC(ctypes.Structure):
+    _fields_ = [
+        ("variant", ctypes.c_int32),
+        ("bisect_iters", ctypes.c_int32),
+        ("liquid_mode", ctypes.c_int32),
+        ("override_flags", ctypes.c_int32),
+        ("reset_mode", ctypes.c_int32),
+        ("reset_epoch", ctypes.c_int32),
+        ("reset_index", ctypes.c_int32),
+        ("reserved0", ctypes.c_int32),
+        ("kappa", ctypes.c_float),
+        ("bond_penalty", ctypes.c_float),
+        ("one_minus_bond_penalty", ctypes.c_float),
+        ("bond_alpha", ctypes.c_float),
+        ("one_minus_bond_alpha", ctypes.c_float),
+        ("alpha_low", ctypes.c_float),
+        ("alpha_high", ctypes.c_float),
+        ("capacity_alpha", ctypes.c_float),
+        ("decay_keep", ctypes.c_float),
+        ("maxint", ctypes.c_float),
+        ("const_a", ctypes.c_float),
+        ("const_b", ctypes.c_float),
+        ("ln_num", ctypes.c_double),
+        ("ln_low", ctypes.c_double),
+        ("override_high", ctypes.c_double),
+        ("override_low", ctypes.c_double),
+        ("reserved1", ctypes.c_double * 2),
+    ]
+
+
+assert ctypes.sizeof(YumaParamsC) == 128, ctypes.sizeof(YumaParamsC)
+
+OUTPUT_FIELDS = (
+    "Dn", "D", "C", "I", "R", "P", "T", "Tv", "Sn", "bond_alpha", "alpha_ab",
+    "Wn", "Wc", "Wb", "B_inst", "B_hist", "B_final",
+)
+
+
+class YumaOutputsC(ctypes.Structure):
+    _fields_ = [(name, ctypes.c_void_p) for name in OUTPUT_FIELDS]
+
+
+_lock = threading.Lock()
+_lib = None
+
+
+def load_library(path: str | None = None):
+    """Load (once) and type the C-ABI library. Raises EngineUnavailable."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        p = path or LIB_PATH
+        if not os.path.exists(p):
+            raise EngineUnavailable(
+                f"{LIB_NAME} not found at {p}; build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+            )
+        try:
+            lib = ctypes.CDLL(p)
+        except OSError as e:  # pragma: no cover - depends on the ROCm runtime
+            raise EngineUnavailable(f"cannot load {p}: {e}") from e
+        vp, i32, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t
+        lib.yuma_workspace_bytes.argtypes = [i32, i32, i32, i32, i32, i32]
+        lib.yuma_workspace_bytes.restype = sz
+        lib.yuma_run.argtypes = [i32, vp, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, sz, i32, vp]
+        lib.yuma_run.restype = i32
+        lib.yuma_run_profiled.argtypes = lib.yuma_run.argtypes + [ctypes.POINTER(ctypes.c_float)]
+        lib.yuma_run_profiled.restype = i32
+        lib.yuma_epoch.argtypes = [i32, vp, i32, i32, i32, vp, vp, vp, vp, vp, vp, sz, vp]
+        lib.yuma_epoch.restype = i32
+        lib.yuma_synth_weights.argtypes = [ctypes.c_uint64, i32, i32, i32, i32, i32, vp, vp]
+        lib.yuma_synth_weights.restype = i32
+        lib.yuma_last_error.argtypes = []
+        lib.yuma_last_error.restype = ctypes.c_char_p
+        lib.yuma_version.argtypes = []
+        lib.yuma_version.restype = ctypes.c_char_p
+        _lib = lib
+        return lib
+
+
+def device() -> torch.device:
+    """The GPU the engine runs on; raises EngineUnavailable without one."""
+    if not torch.cuda.is_available():
+        raise EngineUnavailable("the Yuma HIP engine needs a ROCm GPU (torch.cuda.is_available() is False)")
+    load_library()
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = load_library().yuma_last_error().decode(errors="replace")
+        raise EngineError(f"{what} failed ({rc}): {msg}")
+
+
+def _ptr(t: torch.Tensor | None) -> int | None:
+    return None if t is None else t.data_ptr()
+
+
+# ---------------------------------------------------------------------------
+# parameter marshalling
+# ---------------------------------------------------------------------------
+def bisect_iterations(consensus_precision) -> int:
+    """Trip count of `while (c_high - c_low) > 1 / precision` (yumas.py:201):
+    the interval halves exactly every iteration, independent of the data."""
+    threshold = 1 / consensus_precision
+    hi, lo, n = 1.0, 0.0, 0
+    while (hi - lo) > threshold:
+        hi = (hi + lo) / 2.0
+        n += 1
+        if n > 4096:  # pragma: no cover - nonsensical precision
+            raise ValueError("consensus_precision too large")
+    return n
+
+
+def f32(x) -> float:
+    return float(np.float32(x))
+
+
+def make_params(variant: int, config, *, maxint: int = 2**64 - 1, reset_mode: int = RESET_NONE,
+                reset_epoch: int | None = None, reset_index: int | None = None) -> YumaParamsC:
+    """Flatten a YumaConfig (yumas.py:29-45) into the engine's POD record."""
+    p = YumaParamsC()
+    p.variant = variant
+    p.bisect_iters = bisect_iterations(config.consensus_precision)
+    p.kappa = f32(config.kappa)
+    p.bond_penalty = f32(config.bond_penalty)
+    p.one_minus_bond_penalty = f32(1 - config.bond_penalty)
+    p.bond_alpha = f32(config.bond_alpha)
+    p.one_minus_bond_alpha = f32(1 - config.bond_alpha)
+    p.alpha_low = f32(config.alpha_low)
+    p.alpha_high = f32(config.alpha_high)
+    p.capacity_alpha = f32(config.capacity_alpha)
+    p.decay_keep = f32(1 - config.decay_rate)
+    p.maxint = f32(float(maxint))
+    p.const_a = p.const_b = float("nan")
+    p.override_high = p.override_low = float("nan")
+    p.liquid_mode = LIQUID_OFF
+    uses_liquid = variant in (VARIANT_RUST, VARIANT_YUMA1, VARIANT_YUMA2, VARIANT_YUMA4)
+    if config.liquid_alpha and uses_liquid:
+        # the reference evaluates these when it reaches them (yumas.py:248-251);
+        # math.log raises ValueError for alpha outside (0, 1) exactly as there
+        ln_high = math.log(1 / config.alpha_high - 1)
+        ln_low = math.log(1 / config.alpha_low - 1)
+        p.ln_num = ln_high - ln_low
+        p.ln_low = ln_low
+        hi_o, lo_o = config.override_consensus_high, config.override_consensus_low
+        flags = 0
+        if hi_o is not None:
+            flags |= OVR_HIGH
+            p.override_high = float(hi_o)
+        if lo_o is not None:
+            flags |= OVR_LOW
+            p.override_low = float(lo_o)
+        p.liquid_mode = LIQUID_QUANTILE
+        if hi_o is not None and lo_o is not None:
+            if hi_o == lo_o:  # python comparison, then consensus_high = quantile(.99)
+                flags |= OVR_FORCE_Q99
+            else:  # pure-python a, b (doubles), rounded when they meet C
+                a = (ln_high - ln_low) / (lo_o - hi_o)
+                b = ln_low + a * lo_o
+                p.const_a, p.const_b = f32(a), f32(b)
+                p.liquid_mode = LIQUID_CONST_AB
+        p.override_flags = flags
+    p.reset_mode = reset_mode
+    p.reset_epoch = -1 if reset_epoch is None else int(reset_epoch)
+    p.reset_index = -1 if reset_index is None else int(reset_index)
+    if reset_mode != RESET_NONE and (reset_epoch is None or reset_index is None):
+        p.reset_mode = RESET_NONE  # `epoch == None` never fires in the reference
+    return p
+
+
+def params_tensor(params: list[YumaParamsC], dev: torch.device) -> torch.Tensor:
+    raw = b"".join(bytes(p) for p in params)
+    host = torch.frombuffer(bytearray(raw), dtype=torch.uint8)
+    return host.to(dev)
+
+
+# ---------------------------------------------------------------------------
+# engine calls
+# ---------------------------------------------------------------------------
+@dataclass
+class RunResult:
+    Dn: torch.Tensor                  # [E, N, V]
+    C: torch.Tensor                   # [E, N, M]
+    I: torch.Tensor                   # [E, N, M]
+    B_final: torch.Tensor             # [N, V, M]
+    B_hist: torch.Tensor | None       # [E, N, V, M]
+    extra: dict
+
+
+def _as_dev(x: torch.Tensor, dev) -> torch.Tensor:
+    return x.to(device=dev, dtype=torch.float32).contiguous()
+
+
+def workspace_bytes(variant: int, N: int, E: int, V: int, M: int, full: bool) -> int:
+    return int(load_library().yuma_workspace_bytes(variant, N, E, V, M, 1 if full else 0))
+
+
+def run(variant: int, params: list[YumaParamsC], W: torch.Tensor, S: torch.Tensor,
+        B_init: torch.Tensor | None = None, Wprev_init: torch.Tensor | None = None, *,
+        want_hist: bool = False, want: tuple[str, ...] = (), chunk_epochs: int = 0,
+        workspace: torch.Tensor | None = None, out: dict | None = None,
+        phase_ms: list | None = None) -> RunResult:
+    """E epochs of N scenarios. W [E,N,V,M], S [E,N,V] (raw); optional
+    B_init [N,V,M] and (Yuma2) normalised Wprev_init [N,V,M]."""
+    dev = device()
+    lib = load_library()
+    E, N, V, M = W.shape
+    if S.shape != (E, N, V):
+        raise ValueError(f"S shape {tuple(S.shape)} does not match W {tuple(W.shape)}")
+    if len(params) != N:
+        raise ValueError("one parameter record per scenario is required")
+    W = _as_dev(W, dev)
+    S = _as_dev(S, dev)
+    B_init = None if B_init is None else _as_dev(B_init, dev)
+    Wprev_init = None if Wprev_init is None else _as_dev(Wprev_init, dev)
+    prm = params_tensor(params, dev)
+    o = {} if out is None else dict(out)
+
+    def need(name, shape):
+        if name not in o or o[name] is None:
+            o[name] = torch.empty(shape, dtype=torch.float32, device=dev)
+
+    need("Dn", (E, N, V))
+    need("C", (E, N, M))
+    need("I", (E, N, M))
+    need("B_final", (N, V, M))
+    if want_hist:
+        need("B_hist", (E, N, V, M))
+    shapes = {
+        "D": (E, N, V), "R": (E, N, M), "P": (E, N, M), "T": (E, N, M), "Tv": (E, N, V),
+        "Sn": (E, N, V), "bond_alpha": (E, N, M), "alpha_ab": (E, N, 2),
+        "Wn": (E, N, V, M), "Wc": (E, N, V, M), "Wb": (E, N, V, M), "B_inst": (E, N, V, M),
+    }
+    for name in want:
+        need(name, shapes[name])
+    if "T" in o and "P" not in o:
+        need("P", shapes["P"])
+    full = o.get("Tv") is not None
+    nbytes = workspace_bytes(variant, N, E, V, M, full)
+    if workspace is None or workspace.numel() < nbytes:
+        workspace = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=dev)
+    outs = YumaOutputsC(**{k: _ptr(o.get(k)) for k in OUTPUT_FIELDS})
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    args = (variant, prm.data_ptr(), N, E, V, M, W.data_ptr(), S.data_ptr(),
+            _ptr(B_init), _ptr(Wprev_init), ctypes.addressof(outs),
+            workspace.data_ptr(), workspace.numel(), int(chunk_epochs), stream)
+    if phase_ms is None:
+        _check(lib.yuma_run(*args), "yuma_run")
+    else:  # bench-only: per-phase device time from HIP events (blocks)
+        buf = (ctypes.c_float * len(PHASES))()
+        _check(lib.yuma_run_profiled(*args, buf), "yuma_run_profiled")
+        phase_ms[:] = list(buf)
+    keep = {k: v for k, v in o.items() if k not in ("Dn", "C", "I", "B_final", "B_hist")}
+    # keep inputs alive until the stream has consumed them
+    keep["_inputs"] = (W, S, B_init, Wprev_init, prm, workspace)
+    return RunResult(o["Dn"], o["C"], o["I"], o["B_final"], o.get("B_hist"), keep)
+
+
+def synth_weights(seed: int, E: int, N: int, V: int, M: int, t0: int = 0,
+                  out: torch.Tensor | None = None) -> torch.Tensor:
+    """Device twin of synth.weights (bit-identical)."""
+    dev = device()
+    if out is None:
+        out = torch.empty((E, N, V, M), dtype=torch.float32, device=dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    _check(load_library().yuma_synth_weights(int(seed) & 0xFFFFFFFFFFFFFFFF, E, N, V, M, t0,
+                                             out.data_ptr(), stream), "yuma_synth_weights")
+    return out
+
+
+def version() -> str:
+    return load_library().yuma_version().decode()

@@ -1,0 +1,177 @@
+"""Epoch driver and dividend tables on the MI355X engine.
+
+Drop-in for the reference's _internal/simulation_utils.py:
+  * ``run_simulation`` (reference :26-112) keeps its signature and return
+    value, but the per-epoch Python loop becomes ONE engine call over all
+    epochs (engine.run): no host round trip between epochs, bond resets
+    (:62-88) applied on the device, and the bond history produced in one
+    buffer;
+  * ``run_simulations`` batches many (case, version, config) runs of equal
+    shape into one engine call per variant — the dividend sheet (reference
+    :319-381) packs all its runs this way;
+  * dividends per 1000 tao are derived from the engine's normalised dividends
+    with the reference's own tensor ops and Python-double formula (:95-107).
+"""
+
+from __future__ import annotations
+
+from collections import defaultdict
+from dataclasses import dataclass
+
+import pandas as pd
+import torch
+
+from yuma_simulation._internal import engine
+from yuma_simulation._internal.cases import BaseCase
+from yuma_simulation._internal.charts_utils import _calculate_total_dividends
+from yuma_simulation._internal.yumas import (
+    SimulationHyperparameters,
+    YumaConfig,
+    YumaParams,
+    YumaSimulationNames,
+)
+
+_NAMES = YumaSimulationNames()
+
+# version string -> (engine variant, bond-reset rule); reference dispatch :52-93
+VERSION_TABLE = {
+    _NAMES.YUMA: (engine.VARIANT_YUMA1, engine.RESET_NONE),
+    _NAMES.YUMA_LIQUID: (engine.VARIANT_YUMA1, engine.RESET_NONE),
+    _NAMES.YUMA2: (engine.VARIANT_YUMA2, engine.RESET_NONE),
+    _NAMES.YUMA3: (engine.VARIANT_YUMA3, engine.RESET_NONE),
+    _NAMES.YUMA31: (engine.VARIANT_YUMA3, engine.RESET_ALWAYS),
+    _NAMES.YUMA32: (engine.VARIANT_YUMA3, engine.RESET_IF_ZERO_CONSENSUS),
+    _NAMES.YUMA4: (engine.VARIANT_YUMA4, engine.RESET_IF_ZERO_CONSENSUS),
+    _NAMES.YUMA4_LIQUID: (engine.VARIANT_YUMA4, engine.RESET_IF_ZERO_CONSENSUS),
+    "Yuma 0 (subtensor)": (engine.VARIANT_RUST, engine.RESET_NONE),
+}
+
+
+def resolve_version(yuma_version: str) -> tuple[int, int]:
+    try:
+        return VERSION_TABLE[yuma_version]
+    except (KeyError, TypeError):
+        raise ValueError("Invalid Yuma function.") from None
+
+
+@dataclass
+class SimulationRun:
+    case: BaseCase
+    yuma_version: str
+    yuma_config: YumaConfig
+
+
+def _dividends_per_1000_tao(case: BaseCase, config: YumaConfig, S: torch.Tensor,
+                            Dn: torch.Tensor) -> dict[str, list[float]]:
+    """Reference simulation_utils.py:48-49,95-107 on CPU tensors [E, V]: the
+    same torch ops (so the same fp32 roundings; a GPU `x / 1000.0` would be a
+    reciprocal multiply), then the Python-double ratio. This is O(E*V) output
+    formatting, not the hot path."""
+    stakes_tao = S * config.total_subnet_stake
+    stakes_units = (stakes_tao / 1000.0).tolist()
+    E_i = config.validator_emission_ratio * Dn
+    emission = (E_i * config.total_epoch_emission).tolist()
+    out: dict[str, list[float]] = {v: [] for v in case.validators}
+    for e in range(len(stakes_units)):
+        for i, validator in enumerate(case.validators):
+            stake_unit = float(stakes_units[e][i])
+            emission_i = float(emission[e][i])
+            out[validator].append(emission_i / stake_unit if stake_unit > 1e-6 else 0.0)
+    return out
+
+
+def run_simulations(runs: list[SimulationRun], *, want_bonds: bool = True,
+                    want_incentives: bool = True):
+    """Run many simulations; runs that share (variant, E, V, M) go to the
+    device as one batched engine call. Returns one (dividends, bonds, incentives)
+    tuple per run, in order."""
+    groups: dict[tuple, list[int]] = defaultdict(list)
+    packed = []
+    for k, r in enumerate(runs):
+        variant, reset_mode = resolve_version(r.yuma_version)
+        W = torch.stack(list(r.case.weights_epochs)[: r.case.num_epochs]).to(torch.float32)
+        S = torch.stack(list(r.case.stakes_epochs)[: r.case.num_epochs]).to(torch.float32)
+        packed.append((variant, reset_mode, W, S))
+        groups[(variant,) + tuple(W.shape)].append(k)
+
+    results: list = [None] * len(runs)
+    for (variant, E, V, M), idx in groups.items():
+        params = []
+        for k in idx:
+            r = runs[k]
+            _, reset_mode, _, _ = packed[k]
+            params.append(engine.make_params(variant, r.yuma_config, reset_mode=reset_mode,
+                                             reset_epoch=r.case.reset_bonds_epoch,
+                                             reset_index=r.case.reset_bonds_index))
+        W = torch.stack([packed[k][2] for k in idx], dim=1)  # [E, N, V, M]
+        S = torch.stack([packed[k][3] for k in idx], dim=1)  # [E, N, V]
+        res = engine.run(variant, params, W, S, want_hist=want_bonds)
+        Dn = res.Dn.cpu()
+        hist = res.B_hist.cpu() if want_bonds else None
+        inc = res.I.cpu() if want_incentives else None
+        for j, k in enumerate(idx):
+            r = runs[k]
+            home = packed[k][2].device
+            div = _dividends_per_1000_tao(r.case, r.yuma_config, packed[k][3].cpu(), Dn[:, j])
+            bonds = [hist[e, j].clone().to(home) for e in range(E)] if want_bonds else []
+            incentives = [inc[e, j].clone().to(home) for e in range(E)] if want_incentives else []
+            results[k] = (div, bonds, incentives)
+    return results
+
+
+def run_simulation(
+    case: BaseCase,
+    yuma_version: str,
+    yuma_config: YumaConfig,
+) -> tuple[dict[str, list[float]], list[torch.Tensor], list[torch.Tensor]]:
+    """Runs the Yuma simulation for a given case and Yuma version, returning
+    dividends, bonds and incentive data (reference simulation_utils.py:26-112)."""
+    resolve_version(yuma_version)
+    return run_simulations([SimulationRun(case, yuma_version, yuma_config)])[0]
+
+
+def generate_total_dividends_table(
+    cases: list[BaseCase],
+    yuma_versions: list[tuple[str, YumaParams]],
+    simulation_hyperparameters: SimulationHyperparameters,
+) -> pd.DataFrame:
+    """Total dividends per standardized validator and version (reference
+    simulation_utils.py:319-381). All (case, version) runs are batched."""
+    standardized = ["Validator A", "Validator B", "Validator C"]
+    for case in cases:
+        if len(case.validators) != 3:
+            raise ValueError(f"Case '{case.name}' does not have exactly 3 validators.")
+    runs = [
+        SimulationRun(case, version, YumaConfig(simulation=simulation_hyperparameters, yuma_params=params))
+        for case in cases
+        for version, params in yuma_versions
+    ]
+    results = iter(run_simulations(runs, want_bonds=False, want_incentives=False))
+    rows: list[dict[str, object]] = []
+    for case in cases:
+        mapping = dict(zip(case.validators, standardized))
+        row: dict[str, object] = {"Case": case.name}
+        for version, _ in yuma_versions:
+            dividends, _, _ = next(results)
+            totals, _ = _calculate_total_dividends(
+                validators=case.validators,
+                dividends_per_validator=dividends,
+                base_validator=case.base_validator,
+                num_epochs=case.num_epochs,
+            )
+            by_std = {mapping[v]: totals.get(v, 0.0) for v in case.validators}
+            for std in standardized:
+                row[f"{std} - {version}"] = by_std.get(std, 0.0)
+        rows.append(row)
+    df = pd.DataFrame(rows)
+    columns = ["Case"] + [
+        f"{std} - {version}" for version, _ in yuma_versions for std in standardized
+        if f"{std} - {version}" in df.columns
+    ]
+    return df[columns]
+
+
+from yuma_simulation._internal.html_tables import (  # noqa: E402,F401  (re-exported surface)
+    _generate_draggable_html_table,
+    _generate_ipynb_table,
+)
