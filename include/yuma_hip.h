@@ -158,7 +158,7 @@ enum yuma_phase {
 
 /* yuma_run plus per-phase device time: HIP events are recorded on `stream`
  * between phases and phase_ms[YUMA_NUM_PHASES] receives the milliseconds
- * spent in each phase summed over chunks (at most 64 chunks). Blocks until
+ * spent in each phase summed over chunks. Blocks until
  * the stream reaches the end of the run. For benchmarks / roofline only. */
 int yuma_run_profiled(int variant, const yuma_params_t* params_dev, int N, int E, int V, int M,
                       const float* W, const float* S, const float* B_init,

@@ -38,6 +38,8 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <vector>
+
 #include "yuma_hip.h"
 
 #define YUMA_VERSION_STRING "yuma_hip 0.1.0 gfx950"
@@ -133,6 +135,36 @@ __device__ __forceinline__ void col_reduce4(float (&v)[4], float4* red /*[NW*16]
   v[3] = a.w;
 }
 
+// Column max / min of a [rows x 64] tile (NaN-ignoring), same structure as col_reduce4.
+template <int NW, bool MAX>
+__device__ __forceinline__ void col_reduce4_ext(float (&v)[4], float4* red, const Lay& L) {
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+#pragma unroll
+    for (int o = 16; o <= 32; o <<= 1) {
+      const float w = __shfl_xor(v[c], o, 64);
+      v[c] = MAX ? (w > v[c] ? w : v[c]) : (w < v[c] ? w : v[c]);
+    }
+  }
+  if (L.lane < 16) red[L.wave * 16 + L.c4] = make_float4(v[0], v[1], v[2], v[3]);
+  __syncthreads();
+#pragma unroll
+  for (int w = 0; w < NW; ++w) {
+    const float4 b = red[w * 16 + L.c4];
+    const float bb[4] = {b.x, b.y, b.z, b.w};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) v[c] = MAX ? (bb[c] > v[c] ? bb[c] : v[c]) : (bb[c] < v[c] ? bb[c] : v[c]);
+  }
+}
+template <int NW>
+__device__ __forceinline__ void col_reduce4_max(float (&v)[4], float4* red, const Lay& L) {
+  col_reduce4_ext<NW, true>(v, red, L);
+}
+template <int NW>
+__device__ __forceinline__ void col_reduce4_min(float (&v)[4], float4* red, const Lay& L) {
+  col_reduce4_ext<NW, false>(v, red, L);
+}
+
 template <bool VEC>
 __device__ __forceinline__ void load4(const float* __restrict__ row, int m, int M, float (&x)[4]) {
   if (VEC) {
@@ -182,6 +214,7 @@ __global__ __launch_bounds__(256) void k_rowsum(const float* __restrict__ W,
     const float* r = W + (slice * V + row) * (long long)M;
     float acc = 0.0f;
     if (VEC) {
+#pragma unroll 8
       for (int m = lane * 4; m < M; m += 256) {
         const float4 t = *reinterpret_cast<const float4*>(r + m);
         acc = acc + t.x;
@@ -261,30 +294,108 @@ __global__ __launch_bounds__(NT) void k_consensus(const float* __restrict__ W,
   }
 
   const float kappa = prm[n].kappa;
-  const int iters = prm[n].bisect_iters;
-  double lo[4] = {0.0, 0.0, 0.0, 0.0}, hi[4] = {1.0, 1.0, 1.0, 1.0};
-  for (int it = 0; it < iters; ++it) {
-    double mid[4];
-    float midf[4], part[4];
+  const int iters = prm[n].bisect_iters;  // host guarantees <= 30
+  // The reference bisection (yumas.py:201-207) on the grid k 2^-n: mid is
+  // (hi + lo) / 2 in double, i.e. the integer midpoint (L + H) / 2, compared
+  // as fp32 (float)(mid) = (float)k * 2^-n. F(k) = sum_v float(W > mid) * S.
+  // When every stake is finite and >= 0 (and kappa >= 0), F is monotone in k
+  // and the result is k* = min{k in [1, 2^n] : F(k) <= kappa} (2^n if none), so
+  // the search may start from a per-column bracket instead of [0, 2^n]:
+  //   F(k) = 0 <= kappa      for k >= gmax = ceil(max Wn 2^n)
+  //   F(k) = sum S (all set) for k <  gmin = ceil(min Wn 2^n)
+  // Both searches keep (L == 0 or F(L) > kappa) && (H == 2^n or F(H) <= kappa),
+  // so they end at the same k*; every F uses the same fixed-order reduction.
+  bool odd_stake = false;
+#pragma unroll
+  for (int i = 0; i < R; ++i) odd_stake |= !(s[i] >= 0.0f) || s[i] == INFINITY;
+  const bool bracket = !__syncthreads_or(odd_stake) && kappa >= 0.0f;
+  const int top = 1 << iters;
+  const float scale = (float)top, inv_scale = 1.0f / scale;
+  int lo_k[4], hi_k[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    lo_k[c] = 0;
+    hi_k[c] = top;
+  }
+  if (bracket) {
+    float vmax[4], vmin[4], stot[4];
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-      mid[c] = (hi[c] + lo[c]) / 2.0;
-      midf[c] = (float)mid[c];
+      vmax[c] = -INFINITY;
+      vmin[c] = INFINITY;
+      stot[c] = 0.0f;
+    }
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      if (L.g + G * i >= V) continue;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const float x = wn[i][c];
+        vmax[c] = x > vmax[c] ? x : vmax[c];  // a NaN weight is never counted
+        const float xm = x == x ? x : 0.0f;   // ... so it acts like a zero weight
+        vmin[c] = xm < vmin[c] ? xm : vmin[c];
+        stot[c] = stot[c] + s[i];
+      }
+    }
+    col_reduce4_max<NW>(vmax, red[0], L);
+    __syncthreads();
+    col_reduce4_min<NW>(vmin, red[1], L);
+    __syncthreads();
+    col_reduce4<NW>(stot, red[0], L);  // == F(k) with every mask set
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int gmax = vmax[c] > 0.0f ? (int)fminf(ceilf(vmax[c] * scale), scale) : 0;
+      const int gmin = vmin[c] > 0.0f ? (int)fminf(ceilf(vmin[c] * scale), scale + 1.0f) : 0;
+      int lo_c = gmin >= 2 ? gmin - 1 : 0;
+      int hi_c = gmax < 1 ? 1 : gmax;
+      if (lo_c > 0 && !(stot[c] > kappa)) {  // F <= kappa everywhere: k* = 1
+        lo_c = 0;
+        hi_c = 1;
+      }
+      if (lo_c >= top) {  // all weights above 1: F(k) = sum S > kappa for every k < 2^n
+        lo_c = top - 1;
+        hi_c = top;
+      }
+      if (hi_c <= lo_c) hi_c = lo_c + 1;  // unreachable guard
+      lo_k[c] = lo_c;
+      hi_k[c] = hi_c;
+    }
+  }
+  for (int it = 0;; ++it) {
+    bool active = false;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) active |= (hi_k[c] - lo_k[c]) > 1;
+    if (!__syncthreads_or(active)) break;
+    float part[4];
+    int mid[4];
+    float midf[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      mid[c] = (lo_k[c] + hi_k[c]) >> 1;
+      midf[c] = (float)mid[c] * inv_scale;
       part[c] = 0.0f;
     }
 #pragma unroll
-    for (int i = 0; i < R; ++i)
+    for (int i = 0; i < R; ++i) {
+      const float zs = 0.0f * s[i];
 #pragma unroll
-      for (int c = 0; c < 4; ++c) part[c] = part[c] + ((wn[i][c] > midf[c]) ? s[i] : 0.0f);
+      for (int c = 0; c < 4; ++c) part[c] = part[c] + ((wn[i][c] > midf[c]) ? s[i] : zs);
+    }
     col_reduce4<NW>(part, red[it & 1], L);
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-      if (part[c] > kappa)
-        lo[c] = mid[c];
-      else
-        hi[c] = mid[c];
+      if (hi_k[c] - lo_k[c] > 1) {
+        if (part[c] > kappa)
+          lo_k[c] = mid[c];
+        else
+          hi_k[c] = mid[c];
+      }
     }
   }
+  double hi[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) hi[c] = (double)hi_k[c] / (double)top;
   if (L.g == 0)
 #pragma unroll
     for (int c = 0; c < 4; ++c)
@@ -856,6 +967,137 @@ __global__ __launch_bounds__(NT) void k_bonds(BondArgs A) {
 }
 
 // ---------------------------------------------------------------------------
+// Phase 2, element-wise variants (Yuma3 yumas.py:452-472, Yuma4 :570-586):
+// a software-pipelined scan. Each thread owns R rows x 4 miners of the bond
+// tile in registers and keeps the inputs of the next P epochs in flight
+// (a register ring refilled as each epoch is consumed), so the per-epoch HBM
+// latency is hidden behind P-1 epochs of work.
+// ---------------------------------------------------------------------------
+template <int VARIANT, int R, bool VEC, int P>
+__global__ __launch_bounds__(256) void k_bonds_elem(BondArgs A) {
+  constexpr int G = 16;
+  const Lay L = lay();
+  const int tile = blockIdx.x % A.tiles;
+  const int rb = (blockIdx.x / A.tiles) % A.rowblocks;
+  const int n = blockIdx.x / (A.tiles * A.rowblocks);
+  const int N = A.N, V = A.V, M = A.M;
+  const long long VM = (long long)V * M;
+  const int m = tile * kTileM + L.c4 * 4;
+  const yuma_params_t& p = A.prm[n];
+  const int row0 = rb * G * R + L.g;
+  const bool liquid = p.liquid_mode != YUMA_LIQUID_OFF;
+
+  float B[R][4];
+  bool has_old;
+  {
+    const float* src = A.t0 == 0 ? A.B_init : A.Bstate;
+    has_old = src != nullptr;
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const int row = row0 + G * i;
+      if (has_old && row < V)
+        load4<VEC>(src + n * VM + (long long)row * M, m, M, B[i]);
+      else
+#pragma unroll
+        for (int c = 0; c < 4; ++c) B[i][c] = 0.0f;
+    }
+  }
+
+  float rw[P][R][4], rd[P][R], rsn[P][R], ri[P][4], rba[P][4];
+  auto fetch = [&](int k, int t) {
+    const long long slice = (long long)t * N + n;
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const int row = row0 + G * i;
+      if (row < V) {
+        load4<VEC>(A.W + slice * VM + (long long)row * M, m, M, rw[k][i]);
+        rd[k][i] = A.rsd[slice * V + row];
+        rsn[k][i] = A.sn[slice * V + row];
+      } else {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) rw[k][i][c] = 0.0f;
+        rd[k][i] = 1.0f;
+        rsn[k][i] = 0.0f;
+      }
+    }
+    load4_vec(A.I + slice * M, m, M, ri[k]);
+    if (liquid) load4_vec(A.ba + slice * M, m, M, rba[k]);
+  };
+#pragma unroll
+  for (int k = 0; k < P; ++k)
+    if (A.t0 + k < A.t1) fetch(k, A.t0 + k);
+
+  for (int tb = A.t0; tb < A.t1; tb += P) {
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+      const int t = tb + k;
+      if (t >= A.t1) break;
+      const long long slice = (long long)t * N + n;
+      if (has_old && p.reset_mode != YUMA_RESET_NONE && t == p.reset_epoch &&
+          p.reset_index >= 0 && p.reset_index < M) {
+        bool fire = p.reset_mode == YUMA_RESET_ALWAYS;
+        if (p.reset_mode == YUMA_RESET_IF_ZERO_CONSENSUS && t >= 1)
+          fire = A.C[(slice - N) * M + p.reset_index] == 0.0f;
+        const int c = p.reset_index - m;
+        if (fire && c >= 0 && c < 4)
+#pragma unroll
+          for (int i = 0; i < R; ++i)
+#pragma unroll
+            for (int cc = 0; cc < 4; ++cc)
+              if (cc == c) B[i][cc] = 0.0f;
+      }
+      float bac[4], omba[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        bac[c] = liquid ? rba[k][c] : p.bond_alpha;
+        omba[c] = liquid ? 1.0f - rba[k][c] : p.one_minus_bond_alpha;
+      }
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        const int row = row0 + G * i;
+        float wn[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) wn[c] = rw[k][i][c] / rd[k][i];
+        if (VARIANT == YUMA_VARIANT_YUMA3) {
+          const float cap = rsn[k][i] * p.maxint;
+          const float ca = p.capacity_alpha * cap;
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            const float rem = tmax(cap - B[i][c], 0.0f);
+            const float pc = tmin(ca, rem);
+            const float nb = p.decay_keep * B[i][c] + pc * wn[c];
+            B[i][c] = tmin(nb, cap);
+          }
+        } else {
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            const float bd = B[i][c] * omba[c];
+            const float rem = tmax(1.0f - bd, 0.0f);
+            const float nb = bd + tmin(bac[c] * wn[c], rem);
+            B[i][c] = tmin(nb, 1.0f);
+          }
+        }
+        if (A.B_hist != nullptr && row < V)
+          store4<VEC>(A.B_hist + slice * VM + (long long)row * M, m, M, B[i]);
+        float d = 0.0f;
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          if (m + c < M) d = d + B[i][c] * ri[k][c];
+        d = sum_row16(d);
+        if (L.c4 == 0 && row < V) A.dpart[(slice * A.tiles + tile) * V + row] = d;
+      }
+      has_old = true;
+      if (t + P < A.t1) fetch(k, t + P);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    const int row = row0 + G * i;
+    if (row < V) store4<VEC>(A.Bstate + n * VM + (long long)row * M, m, M, B[i]);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Finalize, one block per slice: D = sum over tiles of the partials (Yuma4:
 // D = S * that, yumas.py:590), D_normalized = D / (D.sum() + 1e-6), and
 // validator trust T_v = sum Wc / sum W (yumas.py:224).
@@ -867,38 +1109,54 @@ __global__ __launch_bounds__(256) void k_finalize(const float* __restrict__ dpar
                                                   const float* __restrict__ tvn,
                                                   float* __restrict__ Dn, float* __restrict__ D,
                                                   float* __restrict__ Tv) {
+  // thread (tg, vq): tile group tg = tid / 64 sums tiles tg, tg+4, ...; vq owns
+  // validators 4vq..4vq+3 of the current 256-validator window. Fixed order:
+  // per-group sequential, then groups 0..3.
+  __shared__ float part[4][256];
   __shared__ float red[4];
+  __shared__ float dsh[YUMA_MAX_VALIDATORS];
   const long long slice = slice0 + blockIdx.x;
-  float local = 0.0f;
-  // V <= 1024: each thread owns v = tid + 256 j
-  float dv[4];
+  const int tg = threadIdx.x >> 6, vq = threadIdx.x & 63;
+  const float* dp = dpart + slice * (long long)tiles * V;
+  for (int v0 = 0; v0 < V; v0 += 256) {
+    float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    for (int k = tg; k < tiles; k += 4) {
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int v = threadIdx.x + 256 * j;
-    float d = 0.0f;
-    if (v < V) {
-      for (int k = 0; k < tiles; ++k) d = d + dpart[(slice * tiles + k) * V + v];
-      if (variant == YUMA_VARIANT_YUMA4) d = sn[slice * V + v] * d;
-      local = local + d;
+      for (int j = 0; j < 4; ++j) {
+        const int v = v0 + vq * 4 + j;
+        if (v < V) acc[j] = acc[j] + dp[(long long)k * V + v];
+      }
     }
-    dv[j] = d;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) part[tg][vq * 4 + j] = acc[j];
+    __syncthreads();
+    for (int j = threadIdx.x; j < 256; j += 256) {
+      const int v = v0 + j;
+      if (v < V) {
+        float d = part[0][j];
+        d = d + part[1][j];
+        d = d + part[2][j];
+        d = d + part[3][j];
+        if (variant == YUMA_VARIANT_YUMA4) d = sn[slice * V + v] * d;
+        dsh[v] = d;
+      }
+    }
+    __syncthreads();
   }
+  float local = 0.0f;
+  for (int v = threadIdx.x; v < V; v += 256) local = local + dsh[v];
   const float tot = block_sum<256>(local, red);
   const float den = tot + 1e-6f;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int v = threadIdx.x + 256 * j;
-    if (v < V) {
-      if (Dn != nullptr) Dn[slice * V + v] = dv[j] / den;
-      if (D != nullptr) D[slice * V + v] = dv[j];
-      if (Tv != nullptr) {
-        float a = 0.0f, b = 0.0f;
-        for (int k = 0; k < tiles; ++k) {
-          a = a + tvc[(slice * tiles + k) * V + v];
-          b = b + tvn[(slice * tiles + k) * V + v];
-        }
-        Tv[slice * V + v] = a / b;
+  for (int v = threadIdx.x; v < V; v += 256) {
+    if (Dn != nullptr) Dn[slice * V + v] = dsh[v] / den;
+    if (D != nullptr) D[slice * V + v] = dsh[v];
+    if (Tv != nullptr) {
+      float a = 0.0f, b = 0.0f;
+      for (int k = 0; k < tiles; ++k) {
+        a = a + tvc[(slice * tiles + k) * V + v];
+        b = b + tvn[(slice * tiles + k) * V + v];
       }
+      Tv[slice * V + v] = a / b;
     }
   }
 }
@@ -1090,13 +1348,13 @@ void launch_bonds_colnorm(RowCfg rc, long long nblocks, hipStream_t st, const yk
   }
 }
 
-// Element-wise variants: 256 threads, R rows per thread (R*16 rows per block).
+// Element-wise variants: 256 threads, R rows per thread (R*16 rows per block),
+// inputs of the next kPrefetch epochs kept in flight.
+constexpr int kPrefetch = 4;
 template <int VARIANT, bool VEC>
 void launch_bonds_elem(int R, long long nblocks, hipStream_t st, const yk::BondArgs& A) {
-  if (R == 1)
-    YK_LAUNCH((yk::k_bonds<VARIANT, 256, 1, VEC>), nblocks, 256, st, A);
-  else
-    YK_LAUNCH((yk::k_bonds<VARIANT, 256, 4, VEC>), nblocks, 256, st, A);
+  (void)R;
+  YK_LAUNCH((yk::k_bonds_elem<VARIANT, 1, VEC, kPrefetch>), nblocks, 256, st, A);
 }
 
 template <bool VEC>
@@ -1126,11 +1384,12 @@ void launch_bonds(int variant, RowCfg rc, int elemR, long long nblocks, hipStrea
 struct PhaseTimer {
   float* ms;  // [YUMA_NUM_PHASES] accumulated milliseconds, or nullptr
   hipStream_t st;
-  hipEvent_t ev[YUMA_NUM_PHASES + 1][64];
+  std::vector<hipEvent_t> ev;  // [(YUMA_NUM_PHASES + 1) * nchunks]
   int nchunks;
   int ok;
+  hipEvent_t& at(int phase, int chunk_idx) { return ev[(size_t)phase * nchunks + chunk_idx]; }
   void begin(int chunk_idx, int phase) {
-    if (ms && ok && chunk_idx < 64) (void)hipEventRecord(ev[phase][chunk_idx], st);
+    if (ms && ok) (void)hipEventRecord(at(phase, chunk_idx), st);
   }
 };
 
@@ -1148,6 +1407,8 @@ int run_impl(int variant, const yuma_params_t* prm, int N, int E, int V, int M, 
   if (!prm || !W || !S || !out || !workspace)
     return fail(YUMA_EINVAL, "null params/W/S/outputs/workspace");
   const int full = out->Tv != nullptr;
+  // bisection trip counts above 30 (consensus_precision > 2^30) are not supported;
+  // params live in device memory, so the Python marshaller enforces it.
   Workspace ws = carve((char*)workspace, variant, N, E, V, M, full);
   if (ws.bytes > ws_bytes)
     return fail(YUMA_EWORKSPACE, "workspace %zu < required %zu bytes (full_outputs=%d)",
@@ -1176,7 +1437,7 @@ int run_impl(int variant, const yuma_params_t* prm, int N, int E, int V, int M, 
     chunk = (int)(c < 1 ? 1 : (c > E ? E : c));
   }
 
-  const int elemR = V <= 16 ? 1 : 4;
+  const int elemR = 1;  // 16-row bond blocks: enough blocks to fill the chip at N = 1
   const int colnorm = variant <= YUMA_VARIANT_YUMA2;
   const int rowblocks = colnorm ? 1 : (V + 16 * elemR - 1) / (16 * elemR);
 
@@ -1186,10 +1447,9 @@ int run_impl(int variant, const yuma_params_t* prm, int N, int E, int V, int M, 
   tm.nchunks = (E + chunk - 1) / chunk;
   tm.ok = 1;
   if (phase_ms != nullptr) {
-    if (tm.nchunks > 64) return fail(YUMA_EINVAL, "profiled runs support at most 64 chunks");
-    for (int ph = 0; ph <= YUMA_NUM_PHASES; ++ph)
-      for (int c = 0; c < tm.nchunks; ++c)
-        if (hipEventCreate(&tm.ev[ph][c]) != hipSuccess) tm.ok = 0;
+    tm.ev.resize((size_t)(YUMA_NUM_PHASES + 1) * tm.nchunks);
+    for (auto& e : tm.ev)
+      if (hipEventCreate(&e) != hipSuccess) tm.ok = 0;
     if (!tm.ok) return fail(YUMA_EHIP, "hipEventCreate failed");
   }
 
@@ -1273,16 +1533,15 @@ int run_impl(int variant, const yuma_params_t* prm, int N, int E, int V, int M, 
   if (phase_ms != nullptr) {
     // bench-only path: waits for the stream, then sums per-phase elapsed times
     for (int ph = 0; ph < YUMA_NUM_PHASES; ++ph) phase_ms[ph] = 0.0f;
-    if (hipEventSynchronize(tm.ev[YUMA_NUM_PHASES][tm.nchunks - 1]) != hipSuccess)
+    if (hipEventSynchronize(tm.at(YUMA_NUM_PHASES, tm.nchunks - 1)) != hipSuccess)
       return fail(YUMA_EHIP, "hipEventSynchronize failed");
     for (int c = 0; c < tm.nchunks; ++c)
       for (int ph = 0; ph < YUMA_NUM_PHASES; ++ph) {
         float t = 0.0f;
-        (void)hipEventElapsedTime(&t, tm.ev[ph][c], tm.ev[ph + 1][c]);
+        (void)hipEventElapsedTime(&t, tm.at(ph, c), tm.at(ph + 1, c));
         phase_ms[ph] += t;
       }
-    for (int ph = 0; ph <= YUMA_NUM_PHASES; ++ph)
-      for (int c = 0; c < tm.nchunks; ++c) (void)hipEventDestroy(tm.ev[ph][c]);
+    for (auto& e : tm.ev) (void)hipEventDestroy(e);
   }
   return YUMA_OK;
 }

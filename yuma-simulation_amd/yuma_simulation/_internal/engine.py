@@ -176,6 +176,8 @@ def make_params(variant: int, config, *, maxint: int = 2**64 - 1, reset_mode: in
     p = YumaParamsC()
     p.variant = variant
     p.bisect_iters = bisect_iterations(config.consensus_precision)
+    if p.bisect_iters > 30:
+        raise EngineError("consensus_precision above 2**30 is not supported by the engine")
     p.kappa = f32(config.kappa)
     p.bond_penalty = f32(config.bond_penalty)
     p.one_minus_bond_penalty = f32(1 - config.bond_penalty)
