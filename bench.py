@@ -184,7 +184,7 @@ def main():
                    phase_ms=buf)
         phases += np.array(buf)
     phases /= args.profile_reps
-    eff_chunk = chunk if chunk > 0 else max(1, min(E, (128 << 20) // (N * V * M * 4)))
+    eff_chunk = chunk if 0 < chunk <= E else E
     units = E * N
     phase_info = {}
     for i, name in enumerate(engine.PHASES):

@@ -1,0 +1,96 @@
+"""Multi-process scenario sharding over torch.distributed (gloo, world_size 2,
+CPU). The engine itself needs a GPU, so the ranks use a CPU stand-in runner
+built on the oracle; what is tested is the distribution logic: shard
+boundaries, per-rank parameter selection, and the rank-ordered gather."""
+
+import os
+import socket
+from types import SimpleNamespace
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import yuma_oracle as orc
+from yuma_simulation._internal import synth
+from yuma_simulation._internal.sharding import run_sharded, shard_range
+from yuma_simulation._internal.yumas import SimulationHyperparameters, YumaConfig, YumaParams
+
+VERSION = "Yuma 4 (Rhef+relative bonds) - liquid alpha on"
+
+
+def oracle_runner(variant, configs, W, S, **_):
+    """CPU stand-in with engine.run's signature/return shape."""
+    outs = [orc.run(VERSION, W[:, j].numpy(), S[:, j].numpy(), cfg) for j, cfg in enumerate(configs)]
+    return SimpleNamespace(
+        Dn=torch.from_numpy(np.stack([o["Dn"] for o in outs], axis=1)),
+        C=torch.from_numpy(np.stack([o["C"] for o in outs], axis=1)),
+        I=torch.from_numpy(np.stack([o["I"] for o in outs], axis=1)),
+        B_final=torch.from_numpy(np.stack([o["B"][-1] for o in outs])),
+    )
+
+
+def configs(n):
+    return [YumaConfig(simulation=SimulationHyperparameters(kappa=0.4 + 0.05 * i),
+                       yuma_params=YumaParams(liquid_alpha=True, bond_alpha=0.025 * (i + 1)))
+            for i in range(n)]
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, n_total, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        E, V, M = 4, 8, 24
+        W = torch.from_numpy(synth.weights(9, E, n_total, V, M))
+        S = torch.from_numpy(synth.stakes(9, E, n_total, V, period=2))
+        mine = shard_range(n_total, world, rank)
+        res = run_sharded(4, configs(n_total), W[:, mine.start:mine.stop], S[:, mine.start:mine.stop],
+                          n_total=n_total, runner=oracle_runner)
+        q.put((rank, res.Dn.numpy(), res.C.numpy(), res.I.numpy(), list(res.local)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n_total", [5, 2])
+def test_scenario_sharding_gloo_world2(n_total):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n_total, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    # unsharded reference of the same scenarios
+    E, V, M = 4, 8, 24
+    W = synth.weights(9, E, n_total, V, M)
+    S = synth.stakes(9, E, n_total, V, period=2)
+    full = oracle_runner(4, configs(n_total), torch.from_numpy(W), torch.from_numpy(S))
+    for rank, Dn, C, I, local in got:
+        assert local == list(shard_range(n_total, world, rank))
+        np.testing.assert_array_equal(Dn, full.Dn.numpy())  # every rank holds all scenarios
+        np.testing.assert_array_equal(C, full.C.numpy())
+        np.testing.assert_array_equal(I, full.I.numpy())
+
+
+def test_shard_range_partitions():
+    for n in range(0, 20):
+        for world in range(1, 9):
+            parts = [shard_range(n, world, r) for r in range(world)]
+            flat = [i for p in parts for i in p]
+            assert flat == list(range(n))
+            sizes = [len(p) for p in parts]
+            assert max(sizes) - min(sizes) <= 1
+    with pytest.raises(ValueError):
+        shard_range(4, 2, 2)

@@ -72,6 +72,32 @@ __device__ __forceinline__ float nan_to_num(float x, float nan_v = 0.0f) {
   return x;
 }
 
+// Correctly rounded a / d for a per-row divisor d with its reciprocal r =
+// RN(1/d) precomputed (one IEEE division per row instead of per element):
+// q = RN(a r); e = fma(-d, q, a) (exact); q' = RN(q + e r) is RN(a/d)
+// (Markstein) as long as nothing underflows or overflows. Guard: |d| and |a|
+// in [2^-60, 2^60] (or a = +-0, where q already carries the right sign); any
+// other operand takes the IEEE division. Checked bitwise against IEEE fp32
+// division on 7.9e8 random pairs (tools/README: divtest).
+struct RowDiv {
+  float d, r;
+  bool ok;
+};
+__device__ __forceinline__ RowDiv row_div(float d) {
+  const float ad = fabsf(d);
+  return {d, 1.0f / d, ad >= 0x1p-60f && ad <= 0x1p60f};
+}
+__device__ __forceinline__ float div_rn(float a, const RowDiv& rd) {
+  const float q = a * rd.r;
+  const float e = fmaf(-rd.d, q, a);
+  const float q1 = fmaf(e, rd.r, q);
+  const float aa = fabsf(a);
+  const bool fast = rd.ok && (aa >= 0x1p-60f && aa <= 0x1p60f);
+  float out = a == 0.0f ? q : q1;
+  if (!(fast || (rd.ok && a == 0.0f))) out = a / rd.d;
+  return out;
+}
+
 // thread -> (row group g, column quad c4). A wave covers 4 row groups x 64
 // columns, so one float4 load instruction moves 4 x 256 contiguous bytes.
 struct Lay {
@@ -182,6 +208,43 @@ __device__ __forceinline__ void load4(const float* __restrict__ row, int m, int 
     for (int c = 0; c < 4; ++c) x[c] = (m + c < M) ? row[m + c] : 0.0f;
   }
 }
+// Branch-free loads: out-of-range rows / columns read a clamped in-range
+// address and are zeroed afterwards, so a thread's loads issue back to back
+// instead of one HBM round trip per (divergent) row.
+template <bool VEC>
+__device__ __forceinline__ void load4c(const float* __restrict__ base, int row, int V, int m,
+                                       int M, float (&x)[4]) {
+  const int rr = row < V ? row : V - 1;
+  const float* r = base + (long long)rr * M;
+  if (VEC) {
+    const int mm = m < M ? m : M - 4;
+    const float4 t = *reinterpret_cast<const float4*>(r + mm);
+    x[0] = t.x;
+    x[1] = t.y;
+    x[2] = t.z;
+    x[3] = t.w;
+  } else {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) x[c] = r[min(m + c, M - 1)];
+  }
+}
+__device__ __forceinline__ void mask4(int row, int V, int m, int M, float (&x)[4]) {
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+    if (row >= V || m + c >= M) x[c] = 0.0f;
+}
+__device__ __forceinline__ void vec4raw(const float* __restrict__ v, int m, int M, float (&x)[4]) {
+#pragma unroll
+  for (int c = 0; c < 4; ++c) x[c] = v[min(m + c, M - 1)];
+}
+__device__ __forceinline__ void vec4c(const float* __restrict__ v, int m, int M, float (&x)[4]) {
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const float t = v[min(m + c, M - 1)];
+    x[c] = m + c < M ? t : 0.0f;
+  }
+}
+
 template <bool VEC>
 __device__ __forceinline__ void store4(float* __restrict__ row, int m, int M, const float (&x)[4]) {
   if (VEC) {
@@ -261,22 +324,22 @@ __global__ __launch_bounds__(NT) void k_consensus(const float* __restrict__ W,
   const int m = tile * kTileM + L.c4 * 4;
   const float* Ws = W + slice * (long long)V * M;
 
-  float wn[R][4], s[R];
+  float wn[R][4], s[R], d[R];
+#pragma unroll
+  for (int i = 0; i < R; ++i) load4c<VEC>(Ws, L.g + G * i, V, m, M, wn[i]);
 #pragma unroll
   for (int i = 0; i < R; ++i) {
-    const int row = L.g + G * i;
-    if (row < V) {
-      float x[4];
-      load4<VEC>(Ws + (long long)row * M, m, M, x);
-      const float d = rsd[slice * V + row];
+    const int rr = min(L.g + G * i, V - 1);
+    d[i] = rsd[slice * V + rr];
+    s[i] = sn[slice * V + rr];
+  }
 #pragma unroll
-      for (int c = 0; c < 4; ++c) wn[i][c] = x[c] / d;
-      s[i] = sn[slice * V + row];
-    } else {
+  for (int i = 0; i < R; ++i) {
+    const RowDiv rdv = row_div(d[i]);
 #pragma unroll
-      for (int c = 0; c < 4; ++c) wn[i][c] = 0.0f;
-      s[i] = 0.0f;
-    }
+    for (int c = 0; c < 4; ++c) wn[i][c] = div_rn(wn[i][c], rdv);
+    mask4(L.g + G * i, V, m, M, wn[i]);
+    if (L.g + G * i >= V) s[i] = 0.0f;
   }
 
   if (Pout != nullptr) {
@@ -600,15 +663,23 @@ __global__ __launch_bounds__(NT) void k_rank(
   load4_vec(C + slice * M, m, M, Cc);
 
   float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  float xw[R][4], dv[R], sv[R];
+#pragma unroll
+  for (int i = 0; i < R; ++i) load4c<VEC>(Ws, L.g + G * i, V, m, M, xw[i]);
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    const int rr = min(L.g + G * i, V - 1);
+    dv[i] = rsd[slice * V + rr];
+    sv[i] = sn[slice * V + rr];
+  }
 #pragma unroll
   for (int i = 0; i < R; ++i) {
     const int row = L.g + G * i;
     if (row >= V) continue;
-    float x[4], wn[4], src[4], wc[4];
-    load4<VEC>(Ws + (long long)row * M, m, M, x);
-    const float d = rsd[slice * V + row];
+    float wn[4], src[4], wc[4];
+    const RowDiv rdv = row_div(dv[i]);
 #pragma unroll
-    for (int c = 0; c < 4; ++c) wn[c] = x[c] / d;
+    for (int c = 0; c < 4; ++c) wn[c] = div_rn(xw[i][c], rdv);
     if (yuma2) {
       if (t == 0) {
         if (Wprev_init != nullptr) {
@@ -620,15 +691,15 @@ __global__ __launch_bounds__(NT) void k_rank(
       } else {
         float xp[4];
         load4<VEC>(W + (slice - N) * VM + (long long)row * M, m, M, xp);
-        const float dp = rsd[(slice - N) * V + row];
+        const RowDiv rdp = row_div(rsd[(slice - N) * V + row]);
 #pragma unroll
-        for (int c = 0; c < 4; ++c) src[c] = xp[c] / dp;
+        for (int c = 0; c < 4; ++c) src[c] = div_rn(xp[c], rdp);
       }
     } else {
 #pragma unroll
       for (int c = 0; c < 4; ++c) src[c] = wn[c];
     }
-    const float s = sn[slice * V + row];
+    const float s = sv[i];
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       wc[c] = tmin(src[c], Cc[c]);
@@ -830,22 +901,22 @@ __global__ __launch_bounds__(NT) void k_bonds(BondArgs A) {
       }
     }
 
-    float wn[R][4], s[R];
+    float wn[R][4], s[R], dd[R];
+#pragma unroll
+    for (int i = 0; i < R; ++i) load4c<VEC>(A.W + slice * VM, row0 + G * i, V, m, M, wn[i]);
 #pragma unroll
     for (int i = 0; i < R; ++i) {
-      const int row = row0 + G * i;
-      if (row < V) {
-        float x[4];
-        load4<VEC>(A.W + slice * VM + (long long)row * M, m, M, x);
-        const float d = A.rsd[slice * V + row];
+      const int rr = min(row0 + G * i, V - 1);
+      dd[i] = A.rsd[slice * V + rr];
+      s[i] = A.sn[slice * V + rr];
+    }
 #pragma unroll
-        for (int c = 0; c < 4; ++c) wn[i][c] = x[c] / d;
-        s[i] = A.sn[slice * V + row];
-      } else {
+    for (int i = 0; i < R; ++i) {
+      const RowDiv rdv = row_div(dd[i]);
 #pragma unroll
-        for (int c = 0; c < 4; ++c) wn[i][c] = 0.0f;
-        s[i] = 0.0f;
-      }
+      for (int c = 0; c < 4; ++c) wn[i][c] = div_rn(wn[i][c], rdv);
+      mask4(row0 + G * i, V, m, M, wn[i]);
+      if (row0 + G * i >= V) s[i] = 0.0f;
     }
 
     if (VARIANT == YUMA_VARIANT_YUMA3) {
@@ -983,9 +1054,14 @@ __global__ __launch_bounds__(256) void k_bonds_elem(BondArgs A) {
   const int N = A.N, V = A.V, M = A.M;
   const long long VM = (long long)V * M;
   const int m = tile * kTileM + L.c4 * 4;
-  const yuma_params_t& p = A.prm[n];
+  // every parameter is read once into registers: a global load inside the
+  // epoch loop would make the compiler drain the prefetch ring (vmcnt(0))
+  const yuma_params_t& pg = A.prm[n];
+  const bool liquid = pg.liquid_mode != YUMA_LIQUID_OFF;
+  const int reset_mode = pg.reset_mode, reset_epoch = pg.reset_epoch, reset_index = pg.reset_index;
+  const float p_bond_alpha = pg.bond_alpha, p_omba = pg.one_minus_bond_alpha;
+  const float p_maxint = pg.maxint, p_capacity_alpha = pg.capacity_alpha, p_decay_keep = pg.decay_keep;
   const int row0 = rb * G * R + L.g;
-  const bool liquid = p.liquid_mode != YUMA_LIQUID_OFF;
 
   float B[R][4];
   bool has_old;
@@ -1008,20 +1084,13 @@ __global__ __launch_bounds__(256) void k_bonds_elem(BondArgs A) {
     const long long slice = (long long)t * N + n;
 #pragma unroll
     for (int i = 0; i < R; ++i) {
-      const int row = row0 + G * i;
-      if (row < V) {
-        load4<VEC>(A.W + slice * VM + (long long)row * M, m, M, rw[k][i]);
-        rd[k][i] = A.rsd[slice * V + row];
-        rsn[k][i] = A.sn[slice * V + row];
-      } else {
-#pragma unroll
-        for (int c = 0; c < 4; ++c) rw[k][i][c] = 0.0f;
-        rd[k][i] = 1.0f;
-        rsn[k][i] = 0.0f;
-      }
+      const int rr = min(row0 + G * i, V - 1);
+      load4c<VEC>(A.W + slice * VM, rr, V, m, M, rw[k][i]);
+      rd[k][i] = A.rsd[slice * V + rr];
+      rsn[k][i] = A.sn[slice * V + rr];
     }
-    load4_vec(A.I + slice * M, m, M, ri[k]);
-    if (liquid) load4_vec(A.ba + slice * M, m, M, rba[k]);
+    vec4raw(A.I + slice * M, m, M, ri[k]);  // columns >= M never reach an output
+    if (liquid) vec4raw(A.ba + slice * M, m, M, rba[k]);
   };
 #pragma unroll
   for (int k = 0; k < P; ++k)
@@ -1033,12 +1102,12 @@ __global__ __launch_bounds__(256) void k_bonds_elem(BondArgs A) {
       const int t = tb + k;
       if (t >= A.t1) break;
       const long long slice = (long long)t * N + n;
-      if (has_old && p.reset_mode != YUMA_RESET_NONE && t == p.reset_epoch &&
-          p.reset_index >= 0 && p.reset_index < M) {
-        bool fire = p.reset_mode == YUMA_RESET_ALWAYS;
-        if (p.reset_mode == YUMA_RESET_IF_ZERO_CONSENSUS && t >= 1)
-          fire = A.C[(slice - N) * M + p.reset_index] == 0.0f;
-        const int c = p.reset_index - m;
+      if (has_old && reset_mode != YUMA_RESET_NONE && t == reset_epoch && reset_index >= 0 &&
+          reset_index < M) {
+        bool fire = reset_mode == YUMA_RESET_ALWAYS;
+        if (reset_mode == YUMA_RESET_IF_ZERO_CONSENSUS && t >= 1)
+          fire = A.C[(slice - N) * M + reset_index] == 0.0f;
+        const int c = reset_index - m;
         if (fire && c >= 0 && c < 4)
 #pragma unroll
           for (int i = 0; i < R; ++i)
@@ -1049,23 +1118,24 @@ __global__ __launch_bounds__(256) void k_bonds_elem(BondArgs A) {
       float bac[4], omba[4];
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
-        bac[c] = liquid ? rba[k][c] : p.bond_alpha;
-        omba[c] = liquid ? 1.0f - rba[k][c] : p.one_minus_bond_alpha;
+        bac[c] = liquid ? rba[k][c] : p_bond_alpha;
+        omba[c] = liquid ? 1.0f - rba[k][c] : p_omba;
       }
 #pragma unroll
       for (int i = 0; i < R; ++i) {
         const int row = row0 + G * i;
         float wn[4];
+        const RowDiv rdv = row_div(rd[k][i]);
 #pragma unroll
-        for (int c = 0; c < 4; ++c) wn[c] = rw[k][i][c] / rd[k][i];
+        for (int c = 0; c < 4; ++c) wn[c] = div_rn(rw[k][i][c], rdv);
         if (VARIANT == YUMA_VARIANT_YUMA3) {
-          const float cap = rsn[k][i] * p.maxint;
-          const float ca = p.capacity_alpha * cap;
+          const float cap = rsn[k][i] * p_maxint;
+          const float ca = p_capacity_alpha * cap;
 #pragma unroll
           for (int c = 0; c < 4; ++c) {
             const float rem = tmax(cap - B[i][c], 0.0f);
             const float pc = tmin(ca, rem);
-            const float nb = p.decay_keep * B[i][c] + pc * wn[c];
+            const float nb = p_decay_keep * B[i][c] + pc * wn[c];
             B[i][c] = tmin(nb, cap);
           }
         } else {
@@ -1431,11 +1501,13 @@ int run_impl(int variant, const yuma_params_t* prm, int N, int E, int V, int M, 
   // with liquid_mode OFF neither write nor read it
   float* ba_buf = out->bond_alpha ? out->bond_alpha : ws.ba;
 
-  if (chunk <= 0) {
-    const long long target = 128ll << 20;  // keep a chunk's W inside the 256 MB MALL
-    long long c = target / ((long long)N * slice_elems * 4);
-    chunk = (int)(c < 1 ? 1 : (c > E ? E : c));
+  if (chunk <= 0 || chunk > E) {
+    // one chunk: streaming re-reads gain only ~10% from the 256 MB MALL on
+    // MI355X (tools/membw: 6.6-7.1 TB/s at 64-256 MB vs 6.44 TB/s from HBM),
+    // less than the per-launch cost of more chunks
+    chunk = E;
   }
+  (void)slice_elems;
 
   const int elemR = 1;  // 16-row bond blocks: enough blocks to fill the chip at N = 1
   const int colnorm = variant <= YUMA_VARIANT_YUMA2;
