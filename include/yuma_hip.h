@@ -153,7 +153,9 @@ enum yuma_phase {
   YUMA_PHASE_INCENTIVE = 4, /* k_incentive: incentive, trust                    */
   YUMA_PHASE_BONDS = 5,     /* k_bonds:     bond recurrence over the chunk      */
   YUMA_PHASE_FINALIZE = 6,  /* k_finalize:  dividends                           */
-  YUMA_NUM_PHASES = 7
+  YUMA_PHASE_FUSED1 = 7,    /* k_phase1:    phases 0,1,2(levels),3 in one W pass  */
+  YUMA_PHASE_LIQUID = 8,    /* k_liquid:    liquid-alpha quantiles (fused path)   */
+  YUMA_NUM_PHASES = 9
 };
 
 /* yuma_run plus per-phase device time: HIP events are recorded on `stream`

@@ -1,0 +1,108 @@
+"""Turn rocprofv3 PMC passes into per-kernel HBM bytes (profiles/pmc_traffic.json).
+
+Two separate counter passes of the same bench command (MI355X_MICROARCH.md
+§HBM: FETCH_SIZE and WRITE_SIZE do not fit one pass):
+
+    rocprofv3 --pmc FETCH_SIZE --kernel-trace -T -f csv -d gpurun_out/pmc_fetch -o fetch -- python3 bench.py ...
+    rocprofv3 --pmc WRITE_SIZE --kernel-trace -T -f csv -d gpurun_out/pmc_write -o write -- python3 bench.py ...
+
+Corrections applied (gfx950, per the guide): FETCH_SIZE and WRITE_SIZE are in
+KiB; FETCH_SIZE reports half the bytes of a wide (16 B/lane) coalesced
+streaming read, so it is doubled (the dominant loads here are float4 streams);
+WRITE_SIZE is exact for 16 B/lane streaming stores. The Infinity Cache is
+counted, not excluded.
+
+    python tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write \
+        --epochs 1000 --scenarios 1 --V 256 --M 4096 --version "Yuma 3 (Rhef)" --history
+"""
+
+from __future__ import annotations
+
+import argparse
+import csv
+import glob
+import json
+import os
+import statistics
+from collections import defaultdict
+
+PHASE_OF = {  # kernel name fragment -> bench phase name
+    "k_rowsum": "rowsum",
+    "k_consensus": "consensus",
+    "k_quantise": "quantise",
+    "k_rank": "rank",
+    "k_incentive": "incentive",
+    "k_bonds": "bonds",
+    "k_finalize": "finalize",
+    "k_phase1": "phase1_fused",
+    "k_liquid": "liquid",
+}
+
+
+def counters(directory: str, name: str) -> dict[str, list[float]]:
+    """kernel phase -> list of per-dispatch counter values (KiB)."""
+    files = glob.glob(os.path.join(directory, "**", "*counter_collection*.csv"), recursive=True)
+    if not files:
+        raise SystemExit(f"no counter_collection csv under {directory}")
+    per_dispatch: dict[tuple, float] = defaultdict(float)
+    kname: dict[tuple, str] = {}
+    for path in files:
+        with open(path) as f:
+            for row in csv.DictReader(f):
+                if row.get("Counter_Name") != name:
+                    continue
+                key = (path, row.get("Dispatch_Id") or row.get("Correlation_Id"))
+                per_dispatch[key] += float(row["Counter_Value"])
+                kname[key] = row.get("Kernel_Name", "")
+    out: dict[str, list[float]] = defaultdict(list)
+    for key, v in per_dispatch.items():
+        for frag, phase in PHASE_OF.items():
+            if frag in kname[key]:
+                out[phase].append(v)
+                break
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("fetch_dir")
+    ap.add_argument("write_dir")
+    ap.add_argument("--epochs", type=int, required=True)
+    ap.add_argument("--scenarios", type=int, default=1)
+    ap.add_argument("--V", type=int, default=256)
+    ap.add_argument("--M", type=int, default=4096)
+    ap.add_argument("--version", default="Yuma 3 (Rhef)")
+    ap.add_argument("--history", action="store_true")
+    ap.add_argument("--out", default=os.path.join(os.path.dirname(__file__), "..", "profiles", "pmc_traffic.json"))
+    a = ap.parse_args()
+    fetch = counters(a.fetch_dir, "FETCH_SIZE")
+    write = counters(a.write_dir, "WRITE_SIZE")
+    units = a.epochs * a.scenarios
+    kernels = {}
+    for phase in sorted(set(fetch) | set(write)):
+        f = statistics.median(fetch[phase]) if fetch.get(phase) else 0.0
+        w = statistics.median(write[phase]) if write.get(phase) else 0.0
+        read_b = 2.0 * f * 1024.0   # gfx950: FETCH_SIZE = half of wide streaming reads
+        write_b = w * 1024.0
+        kernels[phase] = {
+            "fetch_size_kib_raw": f,
+            "write_size_kib": w,
+            "hbm_read_bytes_per_launch": read_b,
+            "hbm_write_bytes_per_launch": write_b,
+            "hbm_bytes_per_launch": read_b + write_b,
+            "hbm_bytes_per_scenario_epoch": (read_b + write_b) / units,
+            "dispatches": [len(fetch.get(phase, [])), len(write.get(phase, []))],
+        }
+    rec = {
+        "workload": {"V": a.V, "M": a.M, "epochs": a.epochs, "version": a.version,
+                     "bond_history": bool(a.history)},
+        "correction": "FETCH_SIZE x2 (gfx950 wide-read half count), KiB -> bytes; WRITE_SIZE as is",
+        "kernels": kernels,
+    }
+    with open(a.out, "w") as f:
+        json.dump(rec, f, indent=1)
+    print(json.dumps(rec, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -36,6 +36,7 @@
 #include <stdarg.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <vector>
@@ -87,15 +88,23 @@ __device__ __forceinline__ RowDiv row_div(float d) {
   const float ad = fabsf(d);
   return {d, 1.0f / d, ad >= 0x1p-60f && ad <= 0x1p60f};
 }
-__device__ __forceinline__ float div_rn(float a, const RowDiv& rd) {
+// Fast path only; `slow` is raised when an operand is outside the guard. The
+// caller redoes the whole tile with IEEE division behind a wave-uniform
+// branch (__any(slow)) so the rare path is never if-converted into the hot one.
+__device__ __forceinline__ float div_fast(float a, const RowDiv& rd, bool& slow) {
   const float q = a * rd.r;
   const float e = fmaf(-rd.d, q, a);
   const float q1 = fmaf(e, rd.r, q);
   const float aa = fabsf(a);
-  const bool fast = rd.ok && (aa >= 0x1p-60f && aa <= 0x1p60f);
-  float out = a == 0.0f ? q : q1;
-  if (!(fast || (rd.ok && a == 0.0f))) out = a / rd.d;
-  return out;
+  slow |= !(rd.ok && ((aa >= 0x1p-60f && aa <= 0x1p60f) || a == 0.0f));
+  return a == 0.0f ? q : q1;
+}
+// a / d exactly as IEEE: fast path, IEEE if outside the guard (used where a
+// per-element branch is cheap: the rare paths themselves)
+__device__ __forceinline__ float div_rn(float a, const RowDiv& rd) {
+  bool slow = false;
+  const float q = div_fast(a, rd, slow);
+  return slow ? a / rd.d : q;
 }
 
 // thread -> (row group g, column quad c4). A wave covers 4 row groups x 64
@@ -333,11 +342,25 @@ __global__ __launch_bounds__(NT) void k_consensus(const float* __restrict__ W,
     d[i] = rsd[slice * V + rr];
     s[i] = sn[slice * V + rr];
   }
+  {
+    bool slow = false;
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const RowDiv rdv = row_div(d[i]);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) wn[i][c] = div_fast(wn[i][c], rdv, slow);
+    }
+    if (__any(slow)) {
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        load4c<VEC>(Ws, L.g + G * i, V, m, M, wn[i]);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) wn[i][c] = wn[i][c] / d[i];
+      }
+    }
+  }
 #pragma unroll
   for (int i = 0; i < R; ++i) {
-    const RowDiv rdv = row_div(d[i]);
-#pragma unroll
-    for (int c = 0; c < 4; ++c) wn[i][c] = div_rn(wn[i][c], rdv);
     mask4(L.g + G * i, V, m, M, wn[i]);
     if (L.g + G * i >= V) s[i] = 0.0f;
   }
@@ -463,6 +486,326 @@ __global__ __launch_bounds__(NT) void k_consensus(const float* __restrict__ W,
 #pragma unroll
     for (int c = 0; c < 4; ++c)
       if (m + c < M) craw[slice * M + m + c] = hi[c];
+}
+
+// ---------------------------------------------------------------------------
+// Wave-owned columns: a 64-miner tile per block, 16 miners per wave, every
+// validator row of those miners in the wave's registers. Lane l owns the
+// column quad cq = l & 3 and the row group rg = l >> 2 (rows rg + 16 i).
+// Column reductions are lane butterflies (xor 4, 8, 16, 32): no LDS, no
+// barriers, and each wave runs its own search loop.
+// ---------------------------------------------------------------------------
+struct WLay {
+  int lane, wave, cq, rg;
+};
+__device__ __forceinline__ WLay wlay() {
+  WLay L;
+  L.lane = threadIdx.x & 63;
+  L.wave = threadIdx.x >> 6;
+  L.cq = L.lane & 3;
+  L.rg = L.lane >> 2;
+  return L;
+}
+__device__ __forceinline__ float wsum16(float x) {  // over the 16 row groups
+  x = x + __shfl_xor(x, 4, 64);
+  x = x + __shfl_xor(x, 8, 64);
+  x = x + __shfl_xor(x, 16, 64);
+  x = x + __shfl_xor(x, 32, 64);
+  return x;
+}
+__device__ __forceinline__ float wmax16(float x) {
+#pragma unroll
+  for (int o = 4; o < 64; o <<= 1) {
+    const float y = __shfl_xor(x, o, 64);
+    x = y > x ? y : x;
+  }
+  return x;
+}
+__device__ __forceinline__ float wmin16(float x) {
+#pragma unroll
+  for (int o = 4; o < 64; o <<= 1) {
+    const float y = __shfl_xor(x, o, 64);
+    x = y < x ? y : x;
+  }
+  return x;
+}
+
+// Load + normalise this lane's R rows x 4 miners of a slice (branch-free).
+template <int R, bool VEC>
+__device__ __forceinline__ void load_norm_w(const float* __restrict__ Ws, const float* rsd_s,
+                                            const float* sn_s, int V, int M, int m, int rg,
+                                            float (&wn)[R][4], float (&s)[R]) {
+  float d[R];
+#pragma unroll
+  for (int i = 0; i < R; ++i) load4c<VEC>(Ws, rg + 16 * i, V, m, M, wn[i]);
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    const int rr = min(rg + 16 * i, V - 1);
+    d[i] = rsd_s[rr];
+    s[i] = sn_s[rr];
+  }
+  bool slow = false;
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    const RowDiv rdv = row_div(d[i]);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) wn[i][c] = div_fast(wn[i][c], rdv, slow);
+  }
+  if (__any(slow)) {  // rare: some operand outside the fast-division guard
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      load4c<VEC>(Ws, rg + 16 * i, V, m, M, wn[i]);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) wn[i][c] = wn[i][c] / d[i];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    mask4(rg + 16 * i, V, m, M, wn[i]);
+    if (rg + 16 * i >= V) s[i] = 0.0f;
+  }
+}
+
+// Consensus (see k_consensus for the search argument), wave-owned columns.
+template <int R, bool VEC>
+__global__ __launch_bounds__(256) void k_consensus_w(const float* __restrict__ W,
+                                                     const float* __restrict__ rsd,
+                                                     const float* __restrict__ sn,
+                                                     const yuma_params_t* __restrict__ prm, int N,
+                                                     int V, int M, long long slice0, int tiles,
+                                                     double* __restrict__ craw,
+                                                     float* __restrict__ Pout) {
+  const WLay L = wlay();
+  const long long slice = slice0 + blockIdx.x / tiles;
+  const int tile = blockIdx.x % tiles;
+  const int n = (int)(slice % N);
+  const int m = tile * kTileM + L.wave * 16 + L.cq * 4;
+  if (tile * kTileM + L.wave * 16 >= M) return;  // whole wave past the last miner
+  float wn[R][4], s[R];
+  load_norm_w<R, VEC>(W + slice * (long long)V * M, rsd + slice * V, sn + slice * V, V, M, m,
+                      L.rg, wn, s);
+  if (Pout != nullptr) {
+    float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int i = 0; i < R; ++i)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) acc[c] = acc[c] + s[i] * wn[i][c];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc[c] = wsum16(acc[c]);
+    if (L.rg == 0)
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        if (m + c < M) Pout[slice * M + m + c] = acc[c];
+  }
+  const float kappa = prm[n].kappa;
+  const int iters = prm[n].bisect_iters;
+  bool odd_stake = false;
+#pragma unroll
+  for (int i = 0; i < R; ++i) odd_stake |= !(s[i] >= 0.0f) || s[i] == INFINITY;
+  // every wave of the slice sees the same stakes, so this is slice-uniform
+  const bool bracket = !__any(odd_stake) && kappa >= 0.0f;
+  const int top = 1 << iters;
+  const float scale = (float)top, inv_scale = 1.0f / scale;
+  int lo_k[4], hi_k[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    lo_k[c] = 0;
+    hi_k[c] = top;
+  }
+  if (bracket) {
+    float vmax[4], vmin[4], stot = 0.0f;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      vmax[c] = -INFINITY;
+      vmin[c] = INFINITY;
+    }
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      if (L.rg + 16 * i >= V) continue;
+      stot = stot + s[i];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const float x = wn[i][c];
+        vmax[c] = x > vmax[c] ? x : vmax[c];
+        const float xm = x == x ? x : 0.0f;
+        vmin[c] = xm < vmin[c] ? xm : vmin[c];
+      }
+    }
+    // F(k) with every mask set, in exactly the order every F below uses
+    stot = wsum16(stot);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      vmax[c] = wmax16(vmax[c]);
+      vmin[c] = wmin16(vmin[c]);
+      const int gmax = vmax[c] > 0.0f ? (int)fminf(ceilf(vmax[c] * scale), scale) : 0;
+      const int gmin = vmin[c] > 0.0f ? (int)fminf(ceilf(vmin[c] * scale), scale + 1.0f) : 0;
+      int lo_c = gmin >= 2 ? gmin - 1 : 0;
+      int hi_c = gmax < 1 ? 1 : gmax;
+      if (lo_c > 0 && !(stot > kappa)) {
+        lo_c = 0;
+        hi_c = 1;
+      }
+      if (lo_c >= top) {
+        lo_c = top - 1;
+        hi_c = top;
+      }
+      if (hi_c <= lo_c) hi_c = lo_c + 1;
+      lo_k[c] = lo_c;
+      hi_k[c] = hi_c;
+    }
+  }
+  for (;;) {
+    bool active = false;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) active |= (hi_k[c] - lo_k[c]) > 1;
+    if (!__any(active)) break;
+    float part[4], midf[4];
+    int mid[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      mid[c] = (lo_k[c] + hi_k[c]) >> 1;
+      midf[c] = (float)mid[c] * inv_scale;
+      part[c] = 0.0f;
+    }
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const float zs = 0.0f * s[i];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) part[c] = part[c] + ((wn[i][c] > midf[c]) ? s[i] : zs);
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      part[c] = wsum16(part[c]);
+      if (hi_k[c] - lo_k[c] > 1) {
+        if (part[c] > kappa)
+          lo_k[c] = mid[c];
+        else
+          hi_k[c] = mid[c];
+      }
+    }
+  }
+  if (L.rg == 0)
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      if (m + c < M) craw[slice * M + m + c] = (double)hi_k[c] / (double)top;
+}
+
+// Clip + rank (yumas.py:214-217; Yuma2 clips W_prev :328), wave-owned columns.
+// rpart[slice][tile] = sum over the tile's 64 miners (wave sums, waves in order).
+template <int R, bool VEC, bool YUMA2, bool FULL>
+__global__ __launch_bounds__(256) void k_rank_w(
+    const float* __restrict__ W, const float* __restrict__ rsd, const float* __restrict__ sn,
+    const float* __restrict__ C, const float* __restrict__ Wprev_init, int yuma2_unused, int N, int V,
+    int M, long long slice0, int tiles, float* __restrict__ Rout, float* __restrict__ rpart,
+    float* __restrict__ Wn_out, float* __restrict__ Wc_out, float* __restrict__ tvc,
+    float* __restrict__ tvn) {
+  __shared__ float wsums[4];
+  const WLay L = wlay();
+  const long long slice = slice0 + blockIdx.x / tiles;
+  const int tile = blockIdx.x % tiles;
+  const int n = (int)(slice % N);
+  const long long t = slice / N;
+  const long long VM = (long long)V * M;
+  const int m = tile * kTileM + L.wave * 16 + L.cq * 4;
+  float wn[R][4], s[R];
+  load_norm_w<R, VEC>(W + slice * VM, rsd + slice * V, sn + slice * V, V, M, m, L.rg, wn, s);
+  float Cc[4];
+  vec4c(C + slice * M, m, M, Cc);
+  float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  // source of the clip: W (or Yuma2's previous normalised W), per row
+  auto source = [&](int i, float (&src)[4]) {
+    const int row = L.rg + 16 * i;
+    if (YUMA2) {
+      if (t == 0) {
+        if (Wprev_init != nullptr) {
+          load4c<VEC>(Wprev_init + n * VM, row, V, m, M, src);
+          mask4(row, V, m, M, src);
+        } else {
+#pragma unroll
+          for (int c = 0; c < 4; ++c) src[c] = wn[i][c];
+        }
+      } else {
+        load4c<VEC>(W + (slice - N) * VM, row, V, m, M, src);
+        const RowDiv rdp = row_div(rsd[(slice - N) * V + min(row, V - 1)]);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) src[c] = div_rn(src[c], rdp);
+        mask4(row, V, m, M, src);
+      }
+    } else {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) src[c] = wn[i][c];
+    }
+  };
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    const int row = L.rg + 16 * i;
+    float src[4], wc[4];
+    source(i, src);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      wc[c] = tmin(src[c], Cc[c]);
+      acc[c] = acc[c] + s[i] * wc[c];
+    }
+    if (FULL && row < V) {
+      if (Wn_out != nullptr) store4<VEC>(Wn_out + slice * VM + (long long)row * M, m, M, wn[i]);
+      if (Wc_out != nullptr) store4<VEC>(Wc_out + slice * VM + (long long)row * M, m, M, wc);
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < 4; ++c) acc[c] = wsum16(acc[c]);
+  if (L.rg == 0)
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      if (m + c < M) Rout[slice * M + m + c] = acc[c];
+  // wave sum of its 16 miners (quads in order 0..3), then waves in order
+  float ws = 0.0f;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) ws = ws + acc[c];
+  ws = ws + __shfl_xor(ws, 1, 64);
+  ws = ws + __shfl_xor(ws, 2, 64);
+  if (L.lane == 0) wsums[L.wave] = ws;
+  if (FULL && tvc != nullptr) {
+    // full-output mode only: validator-trust partials over this tile's 64
+    // miners (quads xor 1, 2; then waves in order via LDS); V <= 256 here
+    __shared__ float tvs[2][4][256];
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const int row = L.rg + 16 * i;
+      float src[4];
+      source(i, src);
+      float a = 0.0f, b = 0.0f;
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        if (m + c < M) {
+          a = a + tmin(src[c], Cc[c]);
+          b = b + wn[i][c];
+        }
+      a = a + __shfl_xor(a, 1, 64);
+      a = a + __shfl_xor(a, 2, 64);
+      b = b + __shfl_xor(b, 1, 64);
+      b = b + __shfl_xor(b, 2, 64);
+      if (L.cq == 0 && row < 256) {
+        tvs[0][L.wave][row] = a;
+        tvs[1][L.wave][row] = b;
+      }
+    }
+    __syncthreads();
+    for (int row = threadIdx.x; row < V && row < 256; row += 256) {
+      float a = tvs[0][0][row], b = tvs[1][0][row];
+      for (int w = 1; w < 4; ++w) {
+        a = a + tvs[0][w][row];
+        b = b + tvs[1][w][row];
+      }
+      tvc[(slice * tiles + tile) * V + row] = a;
+      tvn[(slice * tiles + tile) * V + row] = b;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float r = wsums[0];
+    for (int w = 1; w < 4; ++w) r = r + wsums[w];
+    rpart[slice * tiles + tile] = r;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -737,6 +1080,480 @@ __global__ __launch_bounds__(NT) void k_rank(
 }
 
 // ---------------------------------------------------------------------------
+// Phase 1 fused (rowsum + consensus + quantise + rank in ONE read of W).
+// Work items (slice, 64-miner tile) are dequeued in slice-major order by a
+// persistent grid; each block keeps its W tile in registers across two
+// intra-slice hand-offs:
+//   (1) row-sum partials of every tile -> the last arriving block reduces
+//       them to rs[V] (+ S/sum S) and raises flag_rs;
+//   (2) per-tile sums of C_raw -> the last arriver forms sum C, raises flag_c.
+// Protocol (cdna_hip_programming.md Guideline 16): plain stores, every wave
+// s_waitcnt vmcnt(0), barrier, one lane agent-release + asm wait + relaxed
+// atomic; consumers poll one word relaxed with s_sleep, one agent acquire,
+// wait + barrier, then vector loads. Deadlock-free: a block only waits on its
+// own slice, every item of an earlier slice was dequeued before it, and the
+// host only uses this kernel when tiles <= resident blocks / 2. Spins are
+// bounded (timeout word in the sync block).
+// ---------------------------------------------------------------------------
+struct P1Args {
+  const float* W;
+  const float* S;
+  const yuma_params_t* prm;
+  int N, V, M, tiles, variant;
+  long long slice0, nslices;
+  float* rsd;
+  float* sn;
+  double* craw;
+  float* C;
+  int* qlev;
+  float* R;
+  float* rpart;
+  float* P;
+  float* Wn_out;
+  float* Wc_out;
+  float* tvc;
+  float* tvn;
+  unsigned* sync;    // [nslices][4] cnt_rs, flag_rs, cnt_c, flag_c; then head, timeout
+  float* rowpart;    // [nslices][tiles][V]
+  float* cpart_f;    // [nslices][tiles]
+  double* cpart_d;   // [nslices][tiles]
+  float* sumc_f;     // [nslices]
+  double* sumc_d;    // [nslices]
+};
+
+constexpr unsigned kSpinLimit = 1u << 22;
+
+__device__ __forceinline__ unsigned ld_relaxed(const unsigned* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Hand-off form (MI355X_MICROARCH.md visibility table, row 1): every
+// handed-off word is stored with an agent-scope relaxed atomic store (sc1,
+// write-through) and read with an agent-scope relaxed atomic load (sc1,
+// bypasses L1); every storing wave drains (vmcnt(0)) before the workgroup
+// barrier; one lane then signals with an agent atomic. No release/acquire
+// fences (each one writes back / invalidates a whole cache level).
+template <typename Tv>
+__device__ __forceinline__ void st_sc1(Tv* p, Tv v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <typename Tv>
+__device__ __forceinline__ Tv ld_sc1(const Tv* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// every thread calls; returns the counter value before this block's add
+__device__ __forceinline__ unsigned arrive(unsigned* cnt, unsigned* sh) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0)
+    *sh = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  return *sh;
+}
+__device__ __forceinline__ void acquire_block() {
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler ordering only
+  __syncthreads();
+}
+__device__ __forceinline__ void raise_flag(unsigned* flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void wait_flag(const unsigned* flag, unsigned* timeout) {
+  if (threadIdx.x == 0) {
+    unsigned spins = 0;
+    while (ld_relaxed(flag) == 0u) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++spins > kSpinLimit) {
+        __hip_atomic_store(timeout, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler ordering only
+  __syncthreads();
+}
+
+template <int NT, int R, bool VEC>
+__global__ __launch_bounds__(NT, NT == 256 ? 3 : 1) void k_phase1(P1Args A) {
+  constexpr int NW = NT / 64, G = NT / 16;
+  __shared__ float4 red[2][NW * 16];
+  __shared__ unsigned sh_u;
+  __shared__ float shf[NW];
+  __shared__ double shd[NW];
+  const Lay L = lay();
+  const int V = A.V, M = A.M, T = A.tiles;
+  const long long total = A.nslices * T;
+  unsigned* head = A.sync + 4 * A.nslices;
+  unsigned* timeout = head + 1;
+  const bool rust = A.variant == YUMA_VARIANT_RUST;
+
+  for (;;) {
+    if (threadIdx.x == 0) sh_u = __hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const long long item = sh_u;
+    __syncthreads();
+    if (item >= total) break;
+    const long long ls = item / T;  // slice within the chunk
+    const int tile = (int)(item % T);
+    const long long slice = A.slice0 + ls;
+    const int n = (int)(slice % A.N);
+    const int m = tile * kTileM + L.c4 * 4;
+    unsigned* sy = A.sync + 4 * ls;
+
+    // ---- load the tile (one HBM read of W per element, all loads in flight)
+    float x[R][4];
+#pragma unroll
+    for (int i = 0; i < R; ++i) load4c<VEC>(A.W + slice * (long long)V * M, L.g + G * i, V, m, M, x[i]);
+    // ---- (1) row-sum partials of this tile
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      float a = 0.0f;
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        if (m + c < M) a = a + x[i][c];
+      a = sum_row16(a);
+      const int row = L.g + G * i;
+      if (L.c4 == 0 && row < V) st_sc1(&A.rowpart[(ls * T + tile) * V + row], a);
+    }
+    if (arrive(&sy[0], &sh_u) == (unsigned)(T - 1)) {
+      // last arriver: rs[v] = sum over tiles (tile order), S / sum S
+      acquire_block();
+      for (int v = threadIdx.x; v < V; v += NT) {
+        // 16 loads in flight per batch; sums stay in tile order
+        float a = 0.0f;
+        int k = 0;
+        for (; k + 16 <= T; k += 16) {
+          float t[16];
+#pragma unroll
+          for (int j = 0; j < 16; ++j) t[j] = ld_sc1(&A.rowpart[(ls * T + k + j) * V + v]);
+#pragma unroll
+          for (int j = 0; j < 16; ++j) a = a + t[j];
+        }
+        for (; k < T; ++k) a = a + ld_sc1(&A.rowpart[(ls * T + k) * V + v]);
+        st_sc1(&A.rsd[slice * V + v], a + 1e-6f);
+      }
+      float sacc = 0.0f;
+      for (int v = threadIdx.x; v < V; v += NT) sacc = sacc + A.S[slice * V + v];
+      const float stot = block_sum<NT>(sacc, shf);
+      for (int v = threadIdx.x; v < V; v += NT) st_sc1(&A.sn[slice * V + v], A.S[slice * V + v] / stot);
+      raise_flag(&sy[1]);
+    }
+    wait_flag(&sy[1], timeout);
+
+    // ---- normalise in place (rows, stakes are hand-off data: vector loads
+    // after the acquire)
+    float (&wn)[R][4] = x;
+    float s[R];
+    {
+      float dv[R];
+      bool slow = false;
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        const int rr = min(L.g + G * i, V - 1);
+        dv[i] = ld_sc1(&A.rsd[slice * V + rr]);
+        s[i] = ld_sc1(&A.sn[slice * V + rr]);
+      }
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        const RowDiv rdv = row_div(dv[i]);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) wn[i][c] = div_fast(x[i][c], rdv, slow);
+      }
+      if (__syncthreads_or(slow)) {
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+          load4c<VEC>(A.W + slice * (long long)V * M, L.g + G * i, V, m, M, wn[i]);
+#pragma unroll
+          for (int c = 0; c < 4; ++c) wn[i][c] = wn[i][c] / dv[i];
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        mask4(L.g + G * i, V, m, M, wn[i]);
+        if (L.g + G * i >= V) s[i] = 0.0f;
+      }
+    }
+    if (A.P != nullptr) {
+      float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+      for (int i = 0; i < R; ++i)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[c] = acc[c] + s[i] * wn[i][c];
+      col_reduce4<NW>(acc, red[1], L);
+      if (L.g == 0)
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          if (m + c < M) A.P[slice * M + m + c] = acc[c];
+      __syncthreads();
+    }
+
+    // ---- consensus: bracketed exact search (see k_consensus)
+    const float kappa = A.prm[n].kappa;
+    const int iters = A.prm[n].bisect_iters;
+    int hi_k[4];
+    {
+      bool odd_stake = false;
+#pragma unroll
+      for (int i = 0; i < R; ++i) odd_stake |= !(s[i] >= 0.0f) || s[i] == INFINITY;
+      const bool bracket = !__syncthreads_or(odd_stake) && kappa >= 0.0f;
+      const int top = 1 << iters;
+      const float scale = (float)top, inv_scale = 1.0f / scale;
+      int lo_k[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        lo_k[c] = 0;
+        hi_k[c] = top;
+      }
+      if (bracket) {
+        float vmax[4], vmin[4], stot[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          vmax[c] = -INFINITY;
+          vmin[c] = INFINITY;
+          stot[c] = 0.0f;
+        }
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+          if (L.g + G * i >= V) continue;
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            const float xv = wn[i][c];
+            vmax[c] = xv > vmax[c] ? xv : vmax[c];
+            const float xm = xv == xv ? xv : 0.0f;
+            vmin[c] = xm < vmin[c] ? xm : vmin[c];
+            stot[c] = stot[c] + s[i];
+          }
+        }
+        col_reduce4_max<NW>(vmax, red[0], L);
+        __syncthreads();
+        col_reduce4_min<NW>(vmin, red[1], L);
+        __syncthreads();
+        col_reduce4<NW>(stot, red[0], L);
+        __syncthreads();
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const int gmax = vmax[c] > 0.0f ? (int)fminf(ceilf(vmax[c] * scale), scale) : 0;
+          const int gmin = vmin[c] > 0.0f ? (int)fminf(ceilf(vmin[c] * scale), scale + 1.0f) : 0;
+          int lo_c = gmin >= 2 ? gmin - 1 : 0;
+          int hi_c = gmax < 1 ? 1 : gmax;
+          if (lo_c > 0 && !(stot[c] > kappa)) {
+            lo_c = 0;
+            hi_c = 1;
+          }
+          if (lo_c >= top) {
+            lo_c = top - 1;
+            hi_c = top;
+          }
+          if (hi_c <= lo_c) hi_c = lo_c + 1;
+          lo_k[c] = lo_c;
+          hi_k[c] = hi_c;
+        }
+      }
+      for (int it = 0;; ++it) {
+        bool active = false;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) active |= (hi_k[c] - lo_k[c]) > 1;
+        if (!__syncthreads_or(active)) break;
+        float part[4], midf[4];
+        int mid[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          mid[c] = (lo_k[c] + hi_k[c]) >> 1;
+          midf[c] = (float)mid[c] * inv_scale;
+          part[c] = 0.0f;
+        }
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+          const float zs = 0.0f * s[i];
+#pragma unroll
+          for (int c = 0; c < 4; ++c) part[c] = part[c] + ((wn[i][c] > midf[c]) ? s[i] : zs);
+        }
+        col_reduce4<NW>(part, red[it & 1], L);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          if (hi_k[c] - lo_k[c] > 1) {
+            if (part[c] > kappa)
+              lo_k[c] = mid[c];
+            else
+              hi_k[c] = mid[c];
+          }
+        }
+      }
+      __syncthreads();
+      // C_raw = k 2^-n (exact); tile partial of sum C in a fixed order
+      double cr[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) cr[c] = (double)hi_k[c] / (double)top;
+      if (L.g == 0) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          if (m + c < M) A.craw[slice * M + m + c] = cr[c];
+      }
+      if (rust) {
+        double t = 0.0;
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          if (m + c < M) t = t + cr[c];
+        for (int o = 1; o < 16; o <<= 1) t = t + __shfl_xor(t, o, 64);
+        if (threadIdx.x == 0) st_sc1(&A.cpart_d[ls * T + tile], t);
+      } else {
+        float t = 0.0f;
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          if (m + c < M) t = t + (float)cr[c];
+        t = sum_row16(t);
+        if (threadIdx.x == 0) st_sc1(&A.cpart_f[ls * T + tile], t);
+      }
+      if (arrive(&sy[2], &sh_u) == (unsigned)(T - 1)) {
+        acquire_block();
+        if (threadIdx.x < 64) {  // wave 0: lane-strided partial sums, then a butterfly
+          if (rust) {
+            double a = 0.0;
+            for (int k = threadIdx.x; k < T; k += 64) a = a + ld_sc1(&A.cpart_d[ls * T + k]);
+            a = wave_sum_d(a);
+            if (threadIdx.x == 0) st_sc1(&A.sumc_d[ls], a);
+          } else {
+            float a = 0.0f;
+            for (int k = threadIdx.x; k < T; k += 64) a = a + ld_sc1(&A.cpart_f[ls * T + k]);
+            a = wave_sum(a);
+            if (threadIdx.x == 0) st_sc1(&A.sumc_f[ls], a);
+          }
+        }
+        raise_flag(&sy[3]);
+      }
+      wait_flag(&sy[3], timeout);
+      // quantise own columns (yumas.py:211; YumaRust :97 in fp64)
+      float Cc[4];
+      if (rust) {
+        const double sc = ld_sc1(&A.sumc_d[ls]);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const int lev = (int)(cr[c] / sc * 65535.0);
+          Cc[c] = level_value(lev);
+          if (L.g == 0 && m + c < M) A.qlev[slice * M + m + c] = lev;
+        }
+      } else {
+        const float sc = ld_sc1(&A.sumc_f[ls]);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const int lev = (int)((float)cr[c] / sc * 65535.0f);
+          Cc[c] = level_value(lev);
+          if (L.g == 0 && m + c < M) A.qlev[slice * M + m + c] = lev;
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        if (m + c >= M) Cc[c] = 0.0f;
+      if (L.g == 0)
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          if (m + c < M) A.C[slice * M + m + c] = Cc[c];
+
+      // ---- clip + rank (yumas.py:214-217) and the full-output extras
+      float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        const int row = L.g + G * i;
+        float wc[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          wc[c] = tmin(wn[i][c], Cc[c]);
+          acc[c] = acc[c] + s[i] * wc[c];
+        }
+        if (row < V) {
+          const long long off = slice * (long long)V * M + (long long)row * M;
+          if (A.Wn_out != nullptr) store4<VEC>(A.Wn_out + off, m, M, wn[i]);
+          if (A.Wc_out != nullptr) store4<VEC>(A.Wc_out + off, m, M, wc);
+        }
+        if (A.tvc != nullptr) {
+          float a = 0.0f, b = 0.0f;
+#pragma unroll
+          for (int c = 0; c < 4; ++c)
+            if (m + c < M) {
+              a = a + wc[c];
+              b = b + wn[i][c];
+            }
+          a = sum_row16(a);
+          b = sum_row16(b);
+          if (L.c4 == 0 && row < V) {
+            A.tvc[(slice * T + tile) * V + row] = a;
+            A.tvn[(slice * T + tile) * V + row] = b;
+          }
+        }
+      }
+      col_reduce4<NW>(acc, red[0], L);
+      if (L.g == 0)
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          if (m + c < M) A.R[slice * M + m + c] = acc[c];
+      float ts = 0.0f;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) ts = ts + acc[c];
+      ts = sum_row16(ts);
+      if (threadIdx.x == 0) A.rpart[slice * T + tile] = ts;
+      __syncthreads();
+    }
+    (void)shd;
+  }
+}
+
+// Liquid alpha only (the fused phase 1 already quantised C): quantiles of the
+// levels and bond_alpha[m] (yumas.py:231-253). One block per slice.
+template <int NT>
+__global__ __launch_bounds__(NT) void k_liquid(const yuma_params_t* __restrict__ prm, int N, int M,
+                                               long long slice0, const float* __restrict__ C,
+                                               const int* __restrict__ qlev,
+                                               float* __restrict__ ba, float* __restrict__ scal,
+                                               const float* __restrict__ sumc_f,
+                                               const double* __restrict__ sumc_d, int rust) {
+  __shared__ int hist1[256], hist2[256], bc[4];
+  const long long slice = slice0 + blockIdx.x;
+  const yuma_params_t& p = prm[slice % N];
+  const int* q = qlev + slice * M;
+  float a32 = qnan(), b32 = qnan(), ch = qnan(), cl = qnan();
+  if (p.liquid_mode != YUMA_LIQUID_OFF) {
+    if (p.liquid_mode == YUMA_LIQUID_CONST_AB) {
+      a32 = p.const_a;
+      b32 = p.const_b;
+      ch = (float)p.override_high;
+      cl = (float)p.override_low;
+    } else {
+      for (int j = threadIdx.x; j < 256; j += NT) hist1[j] = 0;
+      __syncthreads();
+      for (int mm = threadIdx.x; mm < M; mm += NT) atomicAdd(&hist1[min(max(q[mm], 0), 65535) >> 8], 1);
+      __syncthreads();
+      const bool H = p.override_flags & YUMA_OVR_HIGH, Lw = p.override_flags & YUMA_OVR_LOW;
+      ch = H ? (float)p.override_high : quantile_of<NT>(q, M, 0.75f, hist1, hist2, bc);
+      cl = Lw ? (float)p.override_low : quantile_of<NT>(q, M, 0.25f, hist1, hist2, bc);
+      const bool eq = (H && Lw) ? (p.override_flags & YUMA_OVR_FORCE_Q99) != 0 : (ch == cl);
+      if (eq) ch = quantile_of<NT>(q, M, 0.99f, hist1, hist2, bc);
+      const float d = cl - ch;
+      const float inv = 1.0f / d;
+      a32 = inv * (float)p.ln_num;
+      b32 = (float)p.ln_low + a32 * cl;
+    }
+    const float e32 = 2.71828182845904523536f;
+    for (int mm = threadIdx.x; mm < M; mm += NT) {
+      const float xx = (-a32) * C[slice * M + mm];
+      const float y = xx + b32;
+      const float pw = powf(e32, y);
+      const float den = 1.0f + pw;
+      const float alpha = 1.0f / den;
+      const float clamped = tmin(tmax(alpha, p.alpha_low), p.alpha_high);
+      ba[slice * M + mm] = 1.0f - clamped;
+    }
+  }
+  if (threadIdx.x == 0) {
+    float* sc = scal + slice * 8;
+    sc[0] = rust ? (float)sumc_d[slice - slice0] : sumc_f[slice - slice0];
+    sc[1] = a32;
+    sc[2] = b32;
+    sc[3] = ch;
+    sc[4] = cl;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Phase 1e, one block per slice: I = nan_to_num(R / R.sum(), 0) and the
 // server trust T = nan_to_num(R / P) (yumas.py:220-223).
 // ---------------------------------------------------------------------------
@@ -910,11 +1727,25 @@ __global__ __launch_bounds__(NT) void k_bonds(BondArgs A) {
       dd[i] = A.rsd[slice * V + rr];
       s[i] = A.sn[slice * V + rr];
     }
+    {
+      bool slow = false;
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        const RowDiv rdv = row_div(dd[i]);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) wn[i][c] = div_fast(wn[i][c], rdv, slow);
+      }
+      if (__syncthreads_or(slow)) {
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+          load4c<VEC>(A.W + slice * VM, row0 + G * i, V, m, M, wn[i]);
+#pragma unroll
+          for (int c = 0; c < 4; ++c) wn[i][c] = wn[i][c] / dd[i];
+        }
+      }
+    }
 #pragma unroll
     for (int i = 0; i < R; ++i) {
-      const RowDiv rdv = row_div(dd[i]);
-#pragma unroll
-      for (int c = 0; c < 4; ++c) wn[i][c] = div_rn(wn[i][c], rdv);
       mask4(row0 + G * i, V, m, M, wn[i]);
       if (row0 + G * i >= V) s[i] = 0.0f;
     }
@@ -1126,8 +1957,13 @@ __global__ __launch_bounds__(256) void k_bonds_elem(BondArgs A) {
         const int row = row0 + G * i;
         float wn[4];
         const RowDiv rdv = row_div(rd[k][i]);
+        bool slow = false;
 #pragma unroll
-        for (int c = 0; c < 4; ++c) wn[c] = div_rn(rw[k][i][c], rdv);
+        for (int c = 0; c < 4; ++c) wn[c] = div_fast(rw[k][i][c], rdv, slow);
+        if (__any(slow)) {
+#pragma unroll
+          for (int c = 0; c < 4; ++c) wn[c] = rw[k][i][c] / rd[k][i];
+        }
         if (VARIANT == YUMA_VARIANT_YUMA3) {
           const float cap = rsn[k][i] * p_maxint;
           const float ca = p_capacity_alpha * cap;
@@ -1305,6 +2141,12 @@ struct Workspace {
   float* tvc;
   float* tvn;
   float* Bstate;
+  unsigned* sync;   // fused phase 1: per-slice counters/flags + head + timeout
+  size_t sync_bytes;
+  double* cpart_d;
+  float* cpart_f;
+  float* sumc_f;
+  double* sumc_d;
   size_t bytes;
 };
 
@@ -1333,6 +2175,12 @@ Workspace carve(char* base, int variant, int N, int E, int V, int M, int full) {
   w.tvc = full ? (float*)take(S * tiles * V * 4) : nullptr;
   w.tvn = full ? (float*)take(S * tiles * V * 4) : nullptr;
   w.Bstate = (float*)take((size_t)N * V * M * 4);
+  w.sync_bytes = ((S * 4 + 4) * 4 + 15) & ~size_t(15);
+  w.sync = (unsigned*)take(w.sync_bytes);
+  w.cpart_d = (double*)take(S * tiles * 8);
+  w.cpart_f = (float*)take(S * tiles * 4);
+  w.sumc_f = (float*)take(S * 4);
+  w.sumc_d = (double*)take(S * 8);
   w.bytes = off;
   return w;
 }
@@ -1355,6 +2203,22 @@ template <bool VEC>
 void launch_consensus(RowCfg rc, long long nblocks, hipStream_t st, const float* W,
                       const float* rsd, const float* sn, const yuma_params_t* prm, int N, int V,
                       int M, long long slice0, int tiles, double* craw, float* P) {
+  switch (rc) {  // wave-owned columns up to 256 validators
+    case RC_256_1:
+      YK_LAUNCH((yk::k_consensus_w<1, VEC>), nblocks, 256, st, W, rsd, sn, prm, N, V, M, slice0,
+                tiles, craw, P);
+      return;
+    case RC_256_4:
+      YK_LAUNCH((yk::k_consensus_w<4, VEC>), nblocks, 256, st, W, rsd, sn, prm, N, V, M, slice0,
+                tiles, craw, P);
+      return;
+    case RC_256_16:
+      YK_LAUNCH((yk::k_consensus_w<16, VEC>), nblocks, 256, st, W, rsd, sn, prm, N, V, M, slice0,
+                tiles, craw, P);
+      return;
+    default:
+      break;
+  }
   switch (rc) {
     case RC_256_1:
       YK_LAUNCH((yk::k_consensus<256, 1, VEC>), nblocks, 256, st, W, rsd, sn, prm, N, V, M,
@@ -1375,11 +2239,76 @@ void launch_consensus(RowCfg rc, long long nblocks, hipStream_t st, const float*
   }
 }
 
+int device_cus() {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus <= 0)
+      cus = 1;
+  }
+  return cus;
+}
+
+template <int NT, int R, bool VEC>
+void launch_phase1_cfg(long long total_items, hipStream_t st, const yk::P1Args& A) {
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, yk::k_phase1<NT, R, VEC>, NT, 0) !=
+          hipSuccess ||
+      per_cu < 1)
+    per_cu = 1;
+  long long grid = (long long)device_cus() * per_cu;
+  if (grid > total_items) grid = total_items;
+  YK_LAUNCH((yk::k_phase1<NT, R, VEC>), grid, NT, st, A);
+}
+template <bool VEC>
+void launch_phase1(RowCfg rc, long long total_items, hipStream_t st, const yk::P1Args& A) {
+  switch (rc) {
+    case RC_256_1:
+      launch_phase1_cfg<256, 1, VEC>(total_items, st, A);
+      break;
+    case RC_256_4:
+      launch_phase1_cfg<256, 4, VEC>(total_items, st, A);
+      break;
+    case RC_256_16:
+      launch_phase1_cfg<256, 16, VEC>(total_items, st, A);
+      break;
+    case RC_1024_16:
+      launch_phase1_cfg<1024, 16, VEC>(total_items, st, A);
+      break;
+  }
+}
+
 template <bool VEC>
 void launch_rank(RowCfg rc, long long nblocks, hipStream_t st, const float* W, const float* rsd,
                  const float* sn, const float* C, const float* Wprev_init, int yuma2, int N,
                  int V, int M, long long slice0, int tiles, float* R, float* rpart, float* Wn,
                  float* Wc, float* tvc, float* tvn) {
+  const bool full = Wn != nullptr || Wc != nullptr || tvc != nullptr;
+  auto go = [&](auto kern) {
+    YK_LAUNCH(kern, nblocks, 256, st, W, rsd, sn, C, Wprev_init, yuma2, N, V, M, slice0, tiles, R,
+              rpart, Wn, Wc, tvc, tvn);
+  };
+#define YK_RANKW(RR)                                                   \
+  if (yuma2) {                                                         \
+    if (full) go(yk::k_rank_w<RR, VEC, true, true>);                   \
+    else go(yk::k_rank_w<RR, VEC, true, false>);                       \
+  } else {                                                             \
+    if (full) go(yk::k_rank_w<RR, VEC, false, true>);                  \
+    else go(yk::k_rank_w<RR, VEC, false, false>);                      \
+  }                                                                    \
+  return;
+  switch (rc) {  // wave-owned columns up to 256 validators
+    case RC_256_1:
+      YK_RANKW(1)
+    case RC_256_4:
+      YK_RANKW(4)
+    case RC_256_16:
+      YK_RANKW(16)
+    default:
+      break;
+  }
   switch (rc) {
     case RC_256_1:
       YK_LAUNCH((yk::k_rank<256, 1, VEC>), nblocks, 256, st, W, rsd, sn, C, Wprev_init, yuma2,
@@ -1449,17 +2378,25 @@ void launch_bonds(int variant, RowCfg rc, int elemR, long long nblocks, hipStrea
   }
 }
 
-// Optional per-phase timing (bench / roofline): HIP events recorded on the
-// launch stream between phases; elapsed times summed over chunks.
+// Optional per-phase timing (bench / roofline): a HIP event is recorded on the
+// launch stream at every phase boundary, labelled with the phase that starts
+// there; each segment's elapsed time goes to its label.
 struct PhaseTimer {
   float* ms;  // [YUMA_NUM_PHASES] accumulated milliseconds, or nullptr
   hipStream_t st;
-  std::vector<hipEvent_t> ev;  // [(YUMA_NUM_PHASES + 1) * nchunks]
-  int nchunks;
-  int ok;
-  hipEvent_t& at(int phase, int chunk_idx) { return ev[(size_t)phase * nchunks + chunk_idx]; }
-  void begin(int chunk_idx, int phase) {
-    if (ms && ok) (void)hipEventRecord(at(phase, chunk_idx), st);
+  std::vector<hipEvent_t> ev;
+  std::vector<int> label;
+  int ok = 1;
+  void mark(int phase) {
+    if (!ms || !ok) return;
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) {
+      ok = 0;
+      return;
+    }
+    (void)hipEventRecord(e, st);
+    ev.push_back(e);
+    label.push_back(phase);
   }
 };
 
@@ -1513,41 +2450,84 @@ int run_impl(int variant, const yuma_params_t* prm, int N, int E, int V, int M, 
   const int colnorm = variant <= YUMA_VARIANT_YUMA2;
   const int rowblocks = colnorm ? 1 : (V + 16 * elemR - 1) / (16 * elemR);
 
+  // fused phase 1: not for Yuma2 (clips the previous epoch's weights) and
+  // only while a slice's tiles fit twice into the co-resident blocks
+  // opt-in (YUMA_FUSED=1): measured slower than the multi-pass path on
+  // MI355X (hand-off latency per slice exceeds the saved W reads)
+  const char* fz = getenv("YUMA_FUSED");
+  const bool fused = variant != YUMA_VARIANT_YUMA2 && tiles * 2 <= device_cus() &&
+                     fz != nullptr && fz[0] == '1';
+
   PhaseTimer tm{};
   tm.ms = phase_ms;
   tm.st = st;
-  tm.nchunks = (E + chunk - 1) / chunk;
-  tm.ok = 1;
-  if (phase_ms != nullptr) {
-    tm.ev.resize((size_t)(YUMA_NUM_PHASES + 1) * tm.nchunks);
-    for (auto& e : tm.ev)
-      if (hipEventCreate(&e) != hipSuccess) tm.ok = 0;
-    if (!tm.ok) return fail(YUMA_EHIP, "hipEventCreate failed");
-  }
 
   for (int c0 = 0, ci = 0; c0 < E; c0 += chunk, ++ci) {
     const int c1 = c0 + chunk < E ? c0 + chunk : E;
     const long long s0 = (long long)c0 * N;
     const long long ns = (long long)(c1 - c0) * N;
     const int rowblocks4 = (V + 3) / 4;
-    tm.begin(ci, 0);
+    if (fused) {
+      tm.mark(YUMA_PHASE_FUSED1);
+      yk::P1Args P{};
+      P.W = W;
+      P.S = S;
+      P.prm = prm;
+      P.N = N;
+      P.V = V;
+      P.M = M;
+      P.tiles = tiles;
+      P.variant = variant;
+      P.slice0 = s0;
+      P.nslices = ns;
+      P.rsd = ws.rsd;
+      P.sn = ws.sn;
+      P.craw = ws.craw;
+      P.C = C;
+      P.qlev = ws.qlev;
+      P.R = out->R ? out->R : ws.R;
+      P.rpart = ws.rpart;
+      P.P = out->P;
+      P.Wn_out = out->Wn;
+      P.Wc_out = out->Wc;
+      P.tvc = ws.tvc;
+      P.tvn = ws.tvn;
+      P.sync = ws.sync;
+      P.rowpart = ws.dpart;  // [ns][tiles][V]: free until the bond phase
+      P.cpart_f = ws.cpart_f;
+      P.cpart_d = ws.cpart_d;
+      P.sumc_f = ws.sumc_f;
+      P.sumc_d = ws.sumc_d;
+      (void)hipMemsetAsync(ws.sync, 0, ws.sync_bytes, st);
+      if (vec)
+        launch_phase1<true>(rc, ns * tiles, st, P);
+      else
+        launch_phase1<false>(rc, ns * tiles, st, P);
+      tm.mark(YUMA_PHASE_LIQUID);
+      YK_LAUNCH(yk::k_liquid<256>, ns, 256, st, prm, N, M, s0, C, ws.qlev, ba_buf, ws.scal,
+                ws.sumc_f, ws.sumc_d, variant == YUMA_VARIANT_RUST ? 1 : 0);
+      tm.mark(4);
+      YK_LAUNCH(yk::k_incentive, ns, 256, st, out->R ? out->R : ws.R, ws.rpart, out->P, M, s0,
+                tiles, I, out->P ? out->T : nullptr, ws.scal);
+    } else {
+    tm.mark(0);
     if (vec)
       YK_LAUNCH(yk::k_rowsum<true>, ns * rowblocks4, 256, st, W, S, V, M, s0, rowblocks4,
                 ws.rsd, ws.sn);
     else
       YK_LAUNCH(yk::k_rowsum<false>, ns * rowblocks4, 256, st, W, S, V, M, s0, rowblocks4,
                 ws.rsd, ws.sn);
-    tm.begin(ci, 1);
+    tm.mark(1);
     if (vec)
       launch_consensus<true>(rc, ns * tiles, st, W, ws.rsd, ws.sn, prm, N, V, M, s0, tiles,
                              ws.craw, out->P);
     else
       launch_consensus<false>(rc, ns * tiles, st, W, ws.rsd, ws.sn, prm, N, V, M, s0, tiles,
                               ws.craw, out->P);
-    tm.begin(ci, 2);
+    tm.mark(2);
     YK_LAUNCH(yk::k_quantise<256>, ns, 256, st, ws.craw, prm, variant, N, M, s0, C, ws.qlev,
               ba_buf, ws.scal);
-    tm.begin(ci, 3);
+    tm.mark(3);
     if (vec)
       launch_rank<true>(rc, ns * tiles, st, W, ws.rsd, ws.sn, C, Wprev_init,
                         variant == YUMA_VARIANT_YUMA2, N, V, M, s0, tiles, out->R ? out->R : ws.R,
@@ -1556,9 +2536,10 @@ int run_impl(int variant, const yuma_params_t* prm, int N, int E, int V, int M, 
       launch_rank<false>(rc, ns * tiles, st, W, ws.rsd, ws.sn, C, Wprev_init,
                          variant == YUMA_VARIANT_YUMA2, N, V, M, s0, tiles,
                          out->R ? out->R : ws.R, ws.rpart, out->Wn, out->Wc, ws.tvc, ws.tvn);
-    tm.begin(ci, 4);
+    tm.mark(4);
     YK_LAUNCH(yk::k_incentive, ns, 256, st, out->R ? out->R : ws.R, ws.rpart, out->P, M, s0,
               tiles, I, out->P ? out->T : nullptr, ws.scal);
+    }
 
     yk::BondArgs A{};
     A.W = W;
@@ -1583,12 +2564,12 @@ int run_impl(int variant, const yuma_params_t* prm, int N, int E, int V, int M, 
     A.t0 = c0;
     A.t1 = c1;
     const long long nb = (long long)N * tiles * rowblocks;
-    tm.begin(ci, 5);
+    tm.mark(5);
     if (vec)
       launch_bonds<true>(variant, rc, elemR, nb, st, A);
     else
       launch_bonds<false>(variant, rc, elemR, nb, st, A);
-    tm.begin(ci, 6);
+    tm.mark(6);
     YK_LAUNCH(yk::k_finalize, ns, 256, st, ws.dpart, ws.sn, variant, V, s0, tiles, ws.tvc,
               ws.tvn, out->Dn, out->D, out->Tv);
     if (out->Sn != nullptr)
@@ -1598,21 +2579,21 @@ int run_impl(int variant, const yuma_params_t* prm, int N, int E, int V, int M, 
       (void)hipMemcpy2DAsync(out->alpha_ab + s0 * 2, 2 * sizeof(float), ws.scal + s0 * 8 + 1,
                              8 * sizeof(float), 2 * sizeof(float), (size_t)ns,
                              hipMemcpyDeviceToDevice, st);
-    tm.begin(ci, YUMA_NUM_PHASES);
+    tm.mark(-1);  // end of chunk
   }
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(YUMA_EHIP, "HIP launch failed: %s", hipGetErrorString(e));
   if (phase_ms != nullptr) {
     // bench-only path: waits for the stream, then sums per-phase elapsed times
     for (int ph = 0; ph < YUMA_NUM_PHASES; ++ph) phase_ms[ph] = 0.0f;
-    if (hipEventSynchronize(tm.at(YUMA_NUM_PHASES, tm.nchunks - 1)) != hipSuccess)
+    if (!tm.ok || tm.ev.empty()) return fail(YUMA_EHIP, "event recording failed");
+    if (hipEventSynchronize(tm.ev.back()) != hipSuccess)
       return fail(YUMA_EHIP, "hipEventSynchronize failed");
-    for (int c = 0; c < tm.nchunks; ++c)
-      for (int ph = 0; ph < YUMA_NUM_PHASES; ++ph) {
-        float t = 0.0f;
-        (void)hipEventElapsedTime(&t, tm.at(ph, c), tm.at(ph + 1, c));
-        phase_ms[ph] += t;
-      }
+    for (size_t i = 0; i + 1 < tm.ev.size(); ++i) {
+      float t = 0.0f;
+      (void)hipEventElapsedTime(&t, tm.ev[i], tm.ev[i + 1]);
+      if (tm.label[i] >= 0 && tm.label[i] < YUMA_NUM_PHASES) phase_ms[tm.label[i]] += t;
+    }
     for (auto& e : tm.ev) (void)hipEventDestroy(e);
   }
   return YUMA_OK;

@@ -28,7 +28,8 @@ _PKG_ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__fi
 LIB_PATH = os.environ.get("YUMA_HIP_LIB", os.path.join(_PKG_ROOT, "lib", LIB_NAME))
 
 VARIANT_RUST, VARIANT_YUMA1, VARIANT_YUMA2, VARIANT_YUMA3, VARIANT_YUMA4 = range(5)
-PHASES = ("rowsum", "consensus", "quantise", "rank", "incentive", "bonds", "finalize")
+PHASES = ("rowsum", "consensus", "quantise", "rank", "incentive", "bonds", "finalize",
+          "phase1_fused", "liquid")
 RESET_NONE, RESET_ALWAYS, RESET_IF_ZERO_CONSENSUS = range(3)
 LIQUID_OFF, LIQUID_QUANTILE, LIQUID_CONST_AB = range(3)
 OVR_HIGH, OVR_LOW, OVR_FORCE_Q99 = 1, 2, 4
