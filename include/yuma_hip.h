@@ -175,6 +175,59 @@ int yuma_epoch(int variant, const yuma_params_t* params_dev, int N, int V, int M
                const yuma_outputs_t* out, void* workspace, size_t workspace_bytes,
                void* stream);
 
+/* ------------------------------------------------------------------------
+ * Miner-column sharding of one wide subnet.
+ *
+ * The reference runs a wide subnet as one Yuma* call per epoch
+ * (yumas.py:399 etc., driven by run_simulation, simulation_utils.py:44-110).
+ * Every cross-miner quantity of that epoch step is a sum over miner columns
+ * (row sums :186, sum C :211, sum R :220, D :261/:474/:589) or a quantile of
+ * C (:231-247), and the bond recurrence is column-local, so a process can own
+ * columns [col0, col0 + M) of an M_total-wide subnet. yuma_shard_stage runs
+ * stage k of the whole E-epoch run on those columns; between stages the
+ * caller combines the per-shard partials of every shard (RCCL all-gather,
+ * summed in shard order) and hands the totals back through `io`:
+ *
+ *   stage 1 -> rowsum_part [E][N][V] = sum over local columns of W
+ *   stage 2 <- rowsum      [E][N][V] = sum over shards of rowsum_part
+ *           -> csum_part   [E][N]    = sum of local C_raw (fp32; YumaRust:
+ *                                      csum_part_d, fp64)
+ *   stage 3 <- csum / csum_d [E][N]
+ *           -> levels      [E][N][M] quantisation levels of local columns
+ *              rsum_part   [E][N]    = sum of local R
+ *   stage 4 <- rsum [E][N]; levels_all [E][N][M_total] (liquid scenarios)
+ *           -> dsum_part   [E][N][V] = sum over local columns of B * I
+ *   stage 5 <- dsum [E][N][V]; writes Dn / D
+ *
+ * Every stage takes the same arguments as yuma_run (W [E][N][V][M] holds the
+ * local columns; outputs are the local columns of the [..][M] outputs) and
+ * the same workspace, which carries state from stage to stage. params must
+ * carry reset_index relative to col0 (reset_mode NONE on shards that do not
+ * own the reset column). validator_trust (out->Tv) is not produced.
+ * ---------------------------------------------------------------------- */
+typedef struct yuma_shard_io {
+  int M_total;             /* global miner count                              */
+  int col0;                /* first global column held by this shard          */
+  float* rowsum_part;      /* stage 1 out                                     */
+  const float* rowsum;     /* stage 2 in                                      */
+  float* csum_part;        /* stage 2 out (not YumaRust)                      */
+  double* csum_part_d;     /* stage 2 out (YumaRust)                          */
+  const float* csum;       /* stage 3, 4 in (not YumaRust)                    */
+  const double* csum_d;    /* stage 3, 4 in (YumaRust)                        */
+  int* levels;             /* stage 3 out                                     */
+  float* rsum_part;        /* stage 3 out                                     */
+  const float* rsum;       /* stage 4 in                                      */
+  const int* levels_all;   /* stage 4 in, required when a scenario is liquid  */
+  float* dsum_part;        /* stage 4 out                                     */
+  const float* dsum;       /* stage 5 in                                      */
+} yuma_shard_io_t;
+
+int yuma_shard_stage(int stage, int variant, const yuma_params_t* params_dev, int N, int E,
+                     int V, int M, const float* W, const float* S, const float* B_init,
+                     const float* Wprev_init, const yuma_shard_io_t* io,
+                     const yuma_outputs_t* out, void* workspace, size_t workspace_bytes,
+                     void* stream);
+
 /* Deterministic synthetic inputs: integer-valued weights whose
  * row sums are exact in fp32. Writes W[e][n][v][m] for epochs t0..t0+E-1.
  * Bit-identical to yuma_simulation._internal.synth.weights (numpy).          */

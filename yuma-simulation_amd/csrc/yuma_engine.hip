@@ -47,7 +47,8 @@
 
 namespace yk {
 
-constexpr int kTileM = 64;       // miner columns per tile: 16 lanes x float4
+constexpr int kTileM = 64;
+typedef float fvec4 __attribute__((ext_vector_type(4)));       // miner columns per tile: 16 lanes x float4
 constexpr int kMaxTiles = 1 << 20;
 
 // ---------------------------------------------------------------------------
@@ -277,7 +278,8 @@ template <bool VEC>
 __global__ __launch_bounds__(256) void k_rowsum(const float* __restrict__ W,
                                                 const float* __restrict__ S, int V, int M,
                                                 long long slice0, int rowblocks,
-                                                float* __restrict__ rsd, float* __restrict__ sn) {
+                                                float* __restrict__ rsd, float* __restrict__ sn,
+                                                int partial) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const long long slice = slice0 + blockIdx.x / rowblocks;
   const int rb = blockIdx.x % rowblocks;
@@ -298,7 +300,8 @@ __global__ __launch_bounds__(256) void k_rowsum(const float* __restrict__ W,
       for (int m = lane; m < M; m += 64) acc = acc + r[m];
     }
     acc = wave_sum(acc);
-    if (lane == 0) rsd[slice * V + row] = acc + 1e-6f;
+    // partial (column shard): the caller sums the shards, then k_add_eps
+    if (lane == 0) rsd[slice * V + row] = partial ? acc : acc + 1e-6f;
   }
   if (rb == 0 && wave == 0) {
     const float* s = S + slice * V;
@@ -490,10 +493,11 @@ __global__ __launch_bounds__(NT) void k_consensus(const float* __restrict__ W,
 
 // ---------------------------------------------------------------------------
 // Wave-owned columns: a 64-miner tile per block, 16 miners per wave, every
-// validator row of those miners in the wave's registers. Lane l owns the
-// column quad cq = l & 3 and the row group rg = l >> 2 (rows rg + 16 i).
-// Column reductions are lane butterflies (xor 4, 8, 16, 32): no LDS, no
-// barriers, and each wave runs its own search loop.
+// validator row of those miners in the wave's registers. Lane l owns the row
+// group rg = l & 15 (rows rg + 16 i) and the column quad cq = l >> 4, so the
+// 16 row groups of a column quad are the 16 lanes of one DPP row: column
+// reductions are 4 DPP-modified adds (no LDS, no barriers), and each wave runs
+// its own search loop.
 // ---------------------------------------------------------------------------
 struct WLay {
   int lane, wave, cq, rg;
@@ -502,31 +506,45 @@ __device__ __forceinline__ WLay wlay() {
   WLay L;
   L.lane = threadIdx.x & 63;
   L.wave = threadIdx.x >> 6;
-  L.cq = L.lane & 3;
-  L.rg = L.lane >> 2;
+  L.cq = L.lane >> 4;
+  L.rg = L.lane & 15;
   return L;
 }
-__device__ __forceinline__ float wsum16(float x) {  // over the 16 row groups
-  x = x + __shfl_xor(x, 4, 64);
-  x = x + __shfl_xor(x, 8, 64);
-  x = x + __shfl_xor(x, 16, 64);
-  x = x + __shfl_xor(x, 32, 64);
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float x) {
+  return __builtin_bit_cast(
+      float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), CTRL, 0xF, 0xF, false));
+}
+// Reduction over the 16 lanes of a DPP row by pairwise exchanges (quad_perm
+// [1,0,3,2], quad_perm [2,3,0,1], row_half_mirror, row_mirror): every step
+// pairs lane i with a partner that pairs back, and a + b == b + a bitwise, so
+// all 16 lanes end with identical bits.
+__device__ __forceinline__ float wsum16(float x) {
+  x = x + dpp_f<0xB1>(x);
+  x = x + dpp_f<0x4E>(x);
+  x = x + dpp_f<0x141>(x);
+  x = x + dpp_f<0x140>(x);
   return x;
 }
+// NaN-free inputs only (callers exclude NaN before reducing)
 __device__ __forceinline__ float wmax16(float x) {
-#pragma unroll
-  for (int o = 4; o < 64; o <<= 1) {
-    const float y = __shfl_xor(x, o, 64);
-    x = y > x ? y : x;
-  }
+  x = fmaxf(x, dpp_f<0xB1>(x));
+  x = fmaxf(x, dpp_f<0x4E>(x));
+  x = fmaxf(x, dpp_f<0x141>(x));
+  x = fmaxf(x, dpp_f<0x140>(x));
   return x;
 }
 __device__ __forceinline__ float wmin16(float x) {
-#pragma unroll
-  for (int o = 4; o < 64; o <<= 1) {
-    const float y = __shfl_xor(x, o, 64);
-    x = y < x ? y : x;
-  }
+  x = fminf(x, dpp_f<0xB1>(x));
+  x = fminf(x, dpp_f<0x4E>(x));
+  x = fminf(x, dpp_f<0x141>(x));
+  x = fminf(x, dpp_f<0x140>(x));
+  return x;
+}
+// sum over the 4 column quads of a wave (lanes l, l^16, l^32, l^48)
+__device__ __forceinline__ float qsum4(float x) {
+  x = x + __shfl_xor(x, 16, 64);
+  x = x + __shfl_xor(x, 32, 64);
   return x;
 }
 
@@ -676,12 +694,9 @@ __global__ __launch_bounds__(256) void k_consensus_w(const float* __restrict__ W
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       part[c] = wsum16(part[c]);
-      if (hi_k[c] - lo_k[c] > 1) {
-        if (part[c] > kappa)
-          lo_k[c] = mid[c];
-        else
-          hi_k[c] = mid[c];
-      }
+      const bool act = hi_k[c] - lo_k[c] > 1, up = part[c] > kappa;
+      lo_k[c] = (act && up) ? mid[c] : lo_k[c];
+      hi_k[c] = (act && !up) ? mid[c] : hi_k[c];
     }
   }
   if (L.rg == 0)
@@ -761,8 +776,7 @@ __global__ __launch_bounds__(256) void k_rank_w(
   float ws = 0.0f;
 #pragma unroll
   for (int c = 0; c < 4; ++c) ws = ws + acc[c];
-  ws = ws + __shfl_xor(ws, 1, 64);
-  ws = ws + __shfl_xor(ws, 2, 64);
+  ws = qsum4(ws);
   if (L.lane == 0) wsums[L.wave] = ws;
   if (FULL && tvc != nullptr) {
     // full-output mode only: validator-trust partials over this tile's 64
@@ -780,10 +794,8 @@ __global__ __launch_bounds__(256) void k_rank_w(
           a = a + tmin(src[c], Cc[c]);
           b = b + wn[i][c];
         }
-      a = a + __shfl_xor(a, 1, 64);
-      a = a + __shfl_xor(a, 2, 64);
-      b = b + __shfl_xor(b, 1, 64);
-      b = b + __shfl_xor(b, 2, 64);
+      a = qsum4(a);
+      b = qsum4(b);
       if (L.cq == 0 && row < 256) {
         tvs[0][L.wave][row] = a;
         tvs[1][L.wave][row] = b;
@@ -902,7 +914,10 @@ __global__ __launch_bounds__(NT) void k_quantise(const double* __restrict__ craw
                                                  int variant, int N, int M, long long slice0,
                                                  float* __restrict__ C, int* __restrict__ qlev,
                                                  float* __restrict__ ba,
-                                                 float* __restrict__ scal) {
+                                                 float* __restrict__ scal,
+                                                 const float* __restrict__ ext_sumf,
+                                                 const double* __restrict__ ext_sumd,
+                                                 int no_liquid) {
   __shared__ float redf[NT / 64];
   __shared__ double redd[NT / 64];
   __shared__ int hist1[256], hist2[256], bc[4];
@@ -914,7 +929,15 @@ __global__ __launch_bounds__(NT) void k_quantise(const double* __restrict__ craw
 
   float sumf = 0.0f;
   double sumd = 0.0;
-  if (variant == YUMA_VARIANT_RUST) {
+  if (ext_sumf != nullptr || ext_sumd != nullptr) {
+    // miner-column shard: sum C over every shard, reduced by the caller
+    if (variant == YUMA_VARIANT_RUST) {
+      sumd = ext_sumd[slice];
+      sumf = (float)sumd;
+    } else {
+      sumf = ext_sumf[slice];
+    }
+  } else if (variant == YUMA_VARIANT_RUST) {
     double acc = 0.0;
     for (int m = threadIdx.x; m < M; m += NT) acc = acc + cr[m];
     sumd = block_sum_d<NT>(acc, redd);
@@ -937,7 +960,8 @@ __global__ __launch_bounds__(NT) void k_quantise(const double* __restrict__ craw
     Cs[m] = level_value(lev);
   }
   float a32 = qnan(), b32 = qnan(), ch = qnan(), cl = qnan();
-  if (p.liquid_mode != YUMA_LIQUID_OFF) {
+  // no_liquid: the quantiles need every shard's levels (k_liquid, later stage)
+  if (p.liquid_mode != YUMA_LIQUID_OFF && !no_liquid) {
     if (p.liquid_mode == YUMA_LIQUID_CONST_AB) {
       a32 = p.const_a;
       b32 = p.const_b;
@@ -1502,14 +1526,14 @@ __global__ __launch_bounds__(NT, NT == 256 ? 3 : 1) void k_phase1(P1Args A) {
 template <int NT>
 __global__ __launch_bounds__(NT) void k_liquid(const yuma_params_t* __restrict__ prm, int N, int M,
                                                long long slice0, const float* __restrict__ C,
-                                               const int* __restrict__ qlev,
+                                               const int* __restrict__ qlev, int Mq,
                                                float* __restrict__ ba, float* __restrict__ scal,
                                                const float* __restrict__ sumc_f,
                                                const double* __restrict__ sumc_d, int rust) {
   __shared__ int hist1[256], hist2[256], bc[4];
   const long long slice = slice0 + blockIdx.x;
   const yuma_params_t& p = prm[slice % N];
-  const int* q = qlev + slice * M;
+  const int* q = qlev + slice * Mq;
   float a32 = qnan(), b32 = qnan(), ch = qnan(), cl = qnan();
   if (p.liquid_mode != YUMA_LIQUID_OFF) {
     if (p.liquid_mode == YUMA_LIQUID_CONST_AB) {
@@ -1517,16 +1541,16 @@ __global__ __launch_bounds__(NT) void k_liquid(const yuma_params_t* __restrict__
       b32 = p.const_b;
       ch = (float)p.override_high;
       cl = (float)p.override_low;
-    } else {
+    } else if (qlev != nullptr) {  // (a shard caller that omits the levels gets NaN alphas)
       for (int j = threadIdx.x; j < 256; j += NT) hist1[j] = 0;
       __syncthreads();
-      for (int mm = threadIdx.x; mm < M; mm += NT) atomicAdd(&hist1[min(max(q[mm], 0), 65535) >> 8], 1);
+      for (int mm = threadIdx.x; mm < Mq; mm += NT) atomicAdd(&hist1[min(max(q[mm], 0), 65535) >> 8], 1);
       __syncthreads();
       const bool H = p.override_flags & YUMA_OVR_HIGH, Lw = p.override_flags & YUMA_OVR_LOW;
-      ch = H ? (float)p.override_high : quantile_of<NT>(q, M, 0.75f, hist1, hist2, bc);
-      cl = Lw ? (float)p.override_low : quantile_of<NT>(q, M, 0.25f, hist1, hist2, bc);
+      ch = H ? (float)p.override_high : quantile_of<NT>(q, Mq, 0.75f, hist1, hist2, bc);
+      cl = Lw ? (float)p.override_low : quantile_of<NT>(q, Mq, 0.25f, hist1, hist2, bc);
       const bool eq = (H && Lw) ? (p.override_flags & YUMA_OVR_FORCE_Q99) != 0 : (ch == cl);
-      if (eq) ch = quantile_of<NT>(q, M, 0.99f, hist1, hist2, bc);
+      if (eq) ch = quantile_of<NT>(q, Mq, 0.99f, hist1, hist2, bc);
       const float d = cl - ch;
       const float inv = 1.0f / d;
       a32 = inv * (float)p.ln_num;
@@ -1562,12 +1586,16 @@ __global__ __launch_bounds__(256) void k_incentive(const float* __restrict__ Rin
                                                    const float* __restrict__ Pin, int M,
                                                    long long slice0, int tiles,
                                                    float* __restrict__ I, float* __restrict__ T,
-                                                   float* __restrict__ scal) {
+                                                   float* __restrict__ scal,
+                                                   const float* __restrict__ ext_rsum) {
   __shared__ float tot;
   const long long slice = slice0 + blockIdx.x;
   if (threadIdx.x == 0) {
     float s = 0.0f;
-    for (int k = 0; k < tiles; ++k) s = s + rpart[slice * tiles + k];
+    if (ext_rsum != nullptr)  // miner-column shard: sum over every shard
+      s = ext_rsum[slice];
+    else
+      for (int k = 0; k < tiles; ++k) s = s + rpart[slice * tiles + k];
     tot = s;
     scal[slice * 8 + 5] = s;
   }
@@ -1875,7 +1903,7 @@ __global__ __launch_bounds__(NT) void k_bonds(BondArgs A) {
 // (a register ring refilled as each epoch is consumed), so the per-epoch HBM
 // latency is hidden behind P-1 epochs of work.
 // ---------------------------------------------------------------------------
-template <int VARIANT, int R, bool VEC, int P>
+template <int VARIANT, int R, bool VEC, int P, bool NTS, bool VECI = false>
 __global__ __launch_bounds__(256) void k_bonds_elem(BondArgs A) {
   constexpr int G = 16;
   const Lay L = lay();
@@ -1920,8 +1948,14 @@ __global__ __launch_bounds__(256) void k_bonds_elem(BondArgs A) {
       rd[k][i] = A.rsd[slice * V + rr];
       rsn[k][i] = A.sn[slice * V + rr];
     }
-    vec4raw(A.I + slice * M, m, M, ri[k]);  // columns >= M never reach an output
-    if (liquid) vec4raw(A.ba + slice * M, m, M, rba[k]);
+    // columns >= M never reach an output
+    if (VECI) {
+      load4c<true>(A.I + slice * M, 0, 1, m, M, ri[k]);
+      if (liquid) load4c<true>(A.ba + slice * M, 0, 1, m, M, rba[k]);
+    } else {
+      vec4raw(A.I + slice * M, m, M, ri[k]);
+      if (liquid) vec4raw(A.ba + slice * M, m, M, rba[k]);
+    }
   };
 #pragma unroll
   for (int k = 0; k < P; ++k)
@@ -1983,8 +2017,17 @@ __global__ __launch_bounds__(256) void k_bonds_elem(BondArgs A) {
             B[i][c] = tmin(nb, 1.0f);
           }
         }
-        if (A.B_hist != nullptr && row < V)
-          store4<VEC>(A.B_hist + slice * VM + (long long)row * M, m, M, B[i]);
+        if (A.B_hist != nullptr && row < V) {
+          float* dst = A.B_hist + slice * VM + (long long)row * M;
+          if (NTS && VEC) {
+            // written once, read by nobody in this run: keep it out of L2/MALL
+            if (m < M)
+              __builtin_nontemporal_store(fvec4{B[i][0], B[i][1], B[i][2], B[i][3]},
+                                          reinterpret_cast<fvec4*>(dst + m));
+          } else {
+            store4<VEC>(dst, m, M, B[i]);
+          }
+        }
         float d = 0.0f;
 #pragma unroll
         for (int c = 0; c < 4; ++c)
@@ -2064,6 +2107,58 @@ __global__ __launch_bounds__(256) void k_finalize(const float* __restrict__ dpar
       }
       Tv[slice * V + v] = a / b;
     }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Miner-column shards: the per-shard partial sums a
+// caller reduces across shards between stages, and the hand-back of the
+// reduced values. Each partial is a fixed-order sum over this shard's columns.
+// ---------------------------------------------------------------------------
+// rsd = (sum of the shards' row sums) + 1e-6 (yumas.py:186)
+__global__ __launch_bounds__(256) void k_add_eps(const float* __restrict__ rowsum, long long n,
+                                                 float* __restrict__ rsd) {
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256)
+    rsd[i] = rowsum[i] + 1e-6f;
+}
+// per slice: sum over this shard's columns of C_raw (fp32; YumaRust fp64)
+__global__ __launch_bounds__(256) void k_csum(const double* __restrict__ craw, int rust, int M,
+                                              float* __restrict__ csum_f,
+                                              double* __restrict__ csum_d) {
+  __shared__ float redf[4];
+  __shared__ double redd[4];
+  const long long slice = blockIdx.x;
+  const double* cr = craw + slice * M;
+  if (rust) {
+    double acc = 0.0;
+    for (int m = threadIdx.x; m < M; m += 256) acc = acc + cr[m];
+    acc = block_sum_d<256>(acc, redd);
+    if (threadIdx.x == 0) csum_d[slice] = acc;
+  } else {
+    float acc = 0.0f;
+    for (int m = threadIdx.x; m < M; m += 256) acc = acc + (float)cr[m];
+    acc = block_sum<256>(acc, redf);
+    if (threadIdx.x == 0) csum_f[slice] = acc;
+  }
+}
+// per slice: sum over this shard's tiles of the rank partials
+__global__ __launch_bounds__(64) void k_rsum(const float* __restrict__ rpart, int tiles,
+                                             float* __restrict__ out) {
+  const long long slice = blockIdx.x;
+  if (threadIdx.x == 0) {
+    float s = 0.0f;
+    for (int k = 0; k < tiles; ++k) s = s + rpart[slice * tiles + k];
+    out[slice] = s;
+  }
+}
+// per slice and validator: sum over this shard's tiles of the dividend partials
+__global__ __launch_bounds__(256) void k_dsum(const float* __restrict__ dpart, int V, int tiles,
+                                              float* __restrict__ out) {
+  const long long slice = blockIdx.x;
+  for (int v = threadIdx.x; v < V; v += 256) {
+    float d = 0.0f;
+    for (int k = 0; k < tiles; ++k) d = d + dpart[(slice * tiles + k) * V + v];
+    out[slice * V + v] = d;
   }
 }
 
@@ -2349,11 +2444,34 @@ void launch_bonds_colnorm(RowCfg rc, long long nblocks, hipStream_t st, const yk
 
 // Element-wise variants: 256 threads, R rows per thread (R*16 rows per block),
 // inputs of the next kPrefetch epochs kept in flight.
-constexpr int kPrefetch = 4;
+// YUMA_BONDS=p4|p8|p4nt|p8nt|p4v selects the prefetch depth / history store
+// policy / float4 incentive loads (A/B knob for tools/ab.sh). The default is
+// the measured best on MI355X: 4 epochs in flight, plain stores, per-column
+// incentive loads (float4 ones measured 10% slower: 1.92 vs 1.74 ms at c2).
+int bonds_knob() {
+  static int knob = -1;
+  if (knob < 0) {
+    const char* e = getenv("YUMA_BONDS");
+    knob = 0;
+    if (e != nullptr) {
+      if (!strcmp(e, "p8")) knob = 1;
+      else if (!strcmp(e, "p4nt")) knob = 2;
+      else if (!strcmp(e, "p8nt")) knob = 3;
+      else if (!strcmp(e, "p4v")) knob = 4;
+    }
+  }
+  return knob;
+}
 template <int VARIANT, bool VEC>
 void launch_bonds_elem(int R, long long nblocks, hipStream_t st, const yk::BondArgs& A) {
   (void)R;
-  YK_LAUNCH((yk::k_bonds_elem<VARIANT, 1, VEC, kPrefetch>), nblocks, 256, st, A);
+  switch (bonds_knob()) {
+    case 1: YK_LAUNCH((yk::k_bonds_elem<VARIANT, 1, VEC, 8, false>), nblocks, 256, st, A); break;
+    case 2: YK_LAUNCH((yk::k_bonds_elem<VARIANT, 1, VEC, 4, true>), nblocks, 256, st, A); break;
+    case 3: YK_LAUNCH((yk::k_bonds_elem<VARIANT, 1, VEC, 8, true>), nblocks, 256, st, A); break;
+    case 4: YK_LAUNCH((yk::k_bonds_elem<VARIANT, 1, VEC, 4, false, VEC>), nblocks, 256, st, A); break;
+    default: YK_LAUNCH((yk::k_bonds_elem<VARIANT, 1, VEC, 4, false>), nblocks, 256, st, A); break;
+  }
 }
 
 template <bool VEC>
@@ -2504,19 +2622,19 @@ int run_impl(int variant, const yuma_params_t* prm, int N, int E, int V, int M, 
       else
         launch_phase1<false>(rc, ns * tiles, st, P);
       tm.mark(YUMA_PHASE_LIQUID);
-      YK_LAUNCH(yk::k_liquid<256>, ns, 256, st, prm, N, M, s0, C, ws.qlev, ba_buf, ws.scal,
+      YK_LAUNCH(yk::k_liquid<256>, ns, 256, st, prm, N, M, s0, C, ws.qlev, M, ba_buf, ws.scal,
                 ws.sumc_f, ws.sumc_d, variant == YUMA_VARIANT_RUST ? 1 : 0);
       tm.mark(4);
       YK_LAUNCH(yk::k_incentive, ns, 256, st, out->R ? out->R : ws.R, ws.rpart, out->P, M, s0,
-                tiles, I, out->P ? out->T : nullptr, ws.scal);
+                tiles, I, out->P ? out->T : nullptr, ws.scal, nullptr);
     } else {
     tm.mark(0);
     if (vec)
       YK_LAUNCH(yk::k_rowsum<true>, ns * rowblocks4, 256, st, W, S, V, M, s0, rowblocks4,
-                ws.rsd, ws.sn);
+                ws.rsd, ws.sn, 0);
     else
       YK_LAUNCH(yk::k_rowsum<false>, ns * rowblocks4, 256, st, W, S, V, M, s0, rowblocks4,
-                ws.rsd, ws.sn);
+                ws.rsd, ws.sn, 0);
     tm.mark(1);
     if (vec)
       launch_consensus<true>(rc, ns * tiles, st, W, ws.rsd, ws.sn, prm, N, V, M, s0, tiles,
@@ -2526,7 +2644,7 @@ int run_impl(int variant, const yuma_params_t* prm, int N, int E, int V, int M, 
                               ws.craw, out->P);
     tm.mark(2);
     YK_LAUNCH(yk::k_quantise<256>, ns, 256, st, ws.craw, prm, variant, N, M, s0, C, ws.qlev,
-              ba_buf, ws.scal);
+              ba_buf, ws.scal, nullptr, nullptr, 0);
     tm.mark(3);
     if (vec)
       launch_rank<true>(rc, ns * tiles, st, W, ws.rsd, ws.sn, C, Wprev_init,
@@ -2538,7 +2656,7 @@ int run_impl(int variant, const yuma_params_t* prm, int N, int E, int V, int M, 
                          out->R ? out->R : ws.R, ws.rpart, out->Wn, out->Wc, ws.tvc, ws.tvn);
     tm.mark(4);
     YK_LAUNCH(yk::k_incentive, ns, 256, st, out->R ? out->R : ws.R, ws.rpart, out->P, M, s0,
-              tiles, I, out->P ? out->T : nullptr, ws.scal);
+              tiles, I, out->P ? out->T : nullptr, ws.scal, nullptr);
     }
 
     yk::BondArgs A{};
@@ -2599,6 +2717,145 @@ int run_impl(int variant, const yuma_params_t* prm, int N, int E, int V, int M, 
   return YUMA_OK;
 }
 
+// One stage of a miner-column-sharded run (yuma_hip.h, yuma_shard_stage): the
+// multi-pass path of run_impl cut at its four cross-miner reductions, over all
+// E epochs at once (one chunk), with the reductions supplied by the caller.
+int shard_stage_impl(int stage, int variant, const yuma_params_t* prm, int N, int E, int V, int M,
+                     const float* W, const float* S, const float* B_init,
+                     const float* Wprev_init, const yuma_shard_io_t* io,
+                     const yuma_outputs_t* out, void* workspace, size_t ws_bytes, void* stream) {
+  if (variant < 0 || variant > 4) return fail(YUMA_EINVAL, "unknown variant %d", variant);
+  if (stage < 1 || stage > 5) return fail(YUMA_EINVAL, "unknown shard stage %d", stage);
+  if (N < 1 || E < 1 || V < 1 || M < 1)
+    return fail(YUMA_EINVAL, "sizes must be positive (N=%d E=%d V=%d M=%d)", N, E, V, M);
+  if (V > YUMA_MAX_VALIDATORS)
+    return fail(YUMA_EUNSUPPORTED, "V=%d exceeds YUMA_MAX_VALIDATORS=%d", V,
+                YUMA_MAX_VALIDATORS);
+  if (!prm || !W || !S || !out || !io || !workspace)
+    return fail(YUMA_EINVAL, "null params/W/S/io/outputs/workspace");
+  if (io->M_total < M || io->col0 < 0 || io->col0 + M > io->M_total)
+    return fail(YUMA_EINVAL, "shard [%d, %d) outside M_total=%d", io->col0, io->col0 + M,
+                io->M_total);
+  if (out->Tv != nullptr) return fail(YUMA_EUNSUPPORTED, "validator_trust is not produced by shards");
+  Workspace ws = carve((char*)workspace, variant, N, E, V, M, 0);
+  if (ws.bytes > ws_bytes)
+    return fail(YUMA_EWORKSPACE, "workspace %zu < required %zu bytes", ws_bytes, ws.bytes);
+  hipStream_t st = (hipStream_t)stream;
+  const int tiles = (M + yk::kTileM - 1) / yk::kTileM;
+  const RowCfg rc = row_cfg(V);
+  const bool rust = variant == YUMA_VARIANT_RUST;
+  bool vec = (M % 4) == 0 && aligned16(W);
+  const float* mats[] = {B_init, Wprev_init, out->Wn, out->Wc, out->Wb, out->B_inst,
+                         out->B_hist, out->B_final};
+  for (const float* p : mats)
+    if (p != nullptr && !aligned16(p)) vec = false;
+  float* C = out->C ? out->C : ws.C;
+  float* I = out->I ? out->I : ws.I;
+  float* R = out->R ? out->R : ws.R;
+  float* Bstate = out->B_final ? out->B_final : ws.Bstate;
+  float* ba_buf = out->bond_alpha ? out->bond_alpha : ws.ba;
+  int* qlev = io->levels ? io->levels : ws.qlev;
+  const long long ns = (long long)E * N;
+  switch (stage) {
+    case 1: {
+      if (!io->rowsum_part) return fail(YUMA_EINVAL, "stage 1 needs io->rowsum_part");
+      const int rb4 = (V + 3) / 4;
+      if (vec)
+        YK_LAUNCH(yk::k_rowsum<true>, ns * rb4, 256, st, W, S, V, M, 0LL, rb4, io->rowsum_part,
+                  ws.sn, 1);
+      else
+        YK_LAUNCH(yk::k_rowsum<false>, ns * rb4, 256, st, W, S, V, M, 0LL, rb4, io->rowsum_part,
+                  ws.sn, 1);
+      break;
+    }
+    case 2: {
+      if (!io->rowsum || (rust ? !io->csum_part_d : !io->csum_part))
+        return fail(YUMA_EINVAL, "stage 2 needs io->rowsum and io->csum_part%s", rust ? "_d" : "");
+      long long nb = (ns * V + 255) / 256;
+      if (nb > 4096) nb = 4096;
+      YK_LAUNCH(yk::k_add_eps, nb, 256, st, io->rowsum, ns * V, ws.rsd);
+      if (vec)
+        launch_consensus<true>(rc, ns * tiles, st, W, ws.rsd, ws.sn, prm, N, V, M, 0LL, tiles,
+                               ws.craw, out->P);
+      else
+        launch_consensus<false>(rc, ns * tiles, st, W, ws.rsd, ws.sn, prm, N, V, M, 0LL, tiles,
+                                ws.craw, out->P);
+      YK_LAUNCH(yk::k_csum, ns, 256, st, ws.craw, rust ? 1 : 0, M, io->csum_part, io->csum_part_d);
+      break;
+    }
+    case 3: {
+      if ((rust ? !io->csum_d : !io->csum) || !io->rsum_part)
+        return fail(YUMA_EINVAL, "stage 3 needs io->csum%s and io->rsum_part", rust ? "_d" : "");
+      YK_LAUNCH(yk::k_quantise<256>, ns, 256, st, ws.craw, prm, variant, N, M, 0LL, C, qlev,
+                ba_buf, ws.scal, rust ? nullptr : io->csum, rust ? io->csum_d : nullptr, 1);
+      if (vec)
+        launch_rank<true>(rc, ns * tiles, st, W, ws.rsd, ws.sn, C, Wprev_init,
+                          variant == YUMA_VARIANT_YUMA2, N, V, M, 0LL, tiles, R, ws.rpart,
+                          out->Wn, out->Wc, nullptr, nullptr);
+      else
+        launch_rank<false>(rc, ns * tiles, st, W, ws.rsd, ws.sn, C, Wprev_init,
+                           variant == YUMA_VARIANT_YUMA2, N, V, M, 0LL, tiles, R, ws.rpart,
+                           out->Wn, out->Wc, nullptr, nullptr);
+      YK_LAUNCH(yk::k_rsum, ns, 64, st, ws.rpart, tiles, io->rsum_part);
+      break;
+    }
+    case 4: {
+      if (!io->rsum || !io->dsum_part || (rust ? !io->csum_d : !io->csum))
+        return fail(YUMA_EINVAL, "stage 4 needs io->rsum, io->csum%s and io->dsum_part",
+                    rust ? "_d" : "");
+      // liquid quantiles over every shard's levels; bond_alpha of local columns
+      YK_LAUNCH(yk::k_liquid<256>, ns, 256, st, prm, N, M, 0LL, C, io->levels_all, io->M_total,
+                ba_buf, ws.scal, rust ? nullptr : io->csum, rust ? io->csum_d : nullptr,
+                rust ? 1 : 0);
+      YK_LAUNCH(yk::k_incentive, ns, 256, st, R, ws.rpart, out->P, M, 0LL, tiles, I,
+                out->P ? out->T : nullptr, ws.scal, io->rsum);
+      yk::BondArgs A{};
+      A.W = W;
+      A.rsd = ws.rsd;
+      A.sn = ws.sn;
+      A.C = C;
+      A.I = I;
+      A.ba = ba_buf;
+      A.prm = prm;
+      A.B_init = B_init;
+      A.Wprev_init = Wprev_init;
+      A.Bstate = Bstate;
+      A.B_hist = out->B_hist;
+      A.Wb_out = out->Wb;
+      A.Binst_out = out->B_inst;
+      A.dpart = ws.dpart;
+      A.N = N;
+      A.V = V;
+      A.M = M;
+      A.tiles = tiles;
+      A.rowblocks = variant <= YUMA_VARIANT_YUMA2 ? 1 : (V + 15) / 16;
+      A.t0 = 0;
+      A.t1 = E;
+      const long long nb = (long long)N * tiles * A.rowblocks;
+      if (vec)
+        launch_bonds<true>(variant, rc, 1, nb, st, A);
+      else
+        launch_bonds<false>(variant, rc, 1, nb, st, A);
+      YK_LAUNCH(yk::k_dsum, ns, 256, st, ws.dpart, V, tiles, io->dsum_part);
+      break;
+    }
+    case 5: {
+      if (!io->dsum) return fail(YUMA_EINVAL, "stage 5 needs io->dsum");
+      YK_LAUNCH(yk::k_finalize, ns, 256, st, io->dsum, ws.sn, variant, V, 0LL, 1, nullptr,
+                nullptr, out->Dn, out->D, nullptr);
+      if (out->Sn != nullptr)
+        (void)hipMemcpyAsync(out->Sn, ws.sn, (size_t)ns * V * 4, hipMemcpyDeviceToDevice, st);
+      if (out->alpha_ab != nullptr)
+        (void)hipMemcpy2DAsync(out->alpha_ab, 2 * sizeof(float), ws.scal + 1, 8 * sizeof(float),
+                               2 * sizeof(float), (size_t)ns, hipMemcpyDeviceToDevice, st);
+      break;
+    }
+  }
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(YUMA_EHIP, "HIP launch failed: %s", hipGetErrorString(e));
+  return YUMA_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -2644,6 +2901,15 @@ int yuma_synth_weights(uint64_t seed, int E, int N, int V, int M, int t0, float*
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(YUMA_EHIP, "HIP launch failed: %s", hipGetErrorString(e));
   return YUMA_OK;
+}
+
+int yuma_shard_stage(int stage, int variant, const yuma_params_t* params_dev, int N, int E,
+                     int V, int M, const float* W, const float* S, const float* B_init,
+                     const float* Wprev_init, const yuma_shard_io_t* io,
+                     const yuma_outputs_t* out, void* workspace, size_t workspace_bytes,
+                     void* stream) {
+  return shard_stage_impl(stage, variant, params_dev, N, E, V, M, W, S, B_init, Wprev_init, io,
+                          out, workspace, workspace_bytes, stream);
 }
 
 const char* yuma_last_error(void) { return g_err; }

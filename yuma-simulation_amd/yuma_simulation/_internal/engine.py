@@ -40,6 +40,7 @@ EXPORTED_SYMBOLS = (
     "yuma_run_profiled",
     "yuma_epoch",
     "yuma_synth_weights",
+    "yuma_shard_stage",
     "yuma_last_error",
     "yuma_version",
 )
@@ -95,6 +96,16 @@ class YumaOutputsC(ctypes.Structure):
     _fields_ = [(name, ctypes.c_void_p) for name in OUTPUT_FIELDS]
 
 
+SHARD_IO_FIELDS = ("rowsum_part", "rowsum", "csum_part", "csum_part_d", "csum", "csum_d",
+                   "levels", "rsum_part", "rsum", "levels_all", "dsum_part", "dsum")
+
+
+class YumaShardIOC(ctypes.Structure):
+    """yuma_shard_io_t (include/yuma_hip.h): two ints, then device pointers."""
+    _fields_ = [("M_total", ctypes.c_int), ("col0", ctypes.c_int)] + [
+        (name, ctypes.c_void_p) for name in SHARD_IO_FIELDS]
+
+
 _lock = threading.Lock()
 _lib = None
 
@@ -123,6 +134,9 @@ def load_library(path: str | None = None):
         lib.yuma_run_profiled.restype = i32
         lib.yuma_epoch.argtypes = [i32, vp, i32, i32, i32, vp, vp, vp, vp, vp, vp, sz, vp]
         lib.yuma_epoch.restype = i32
+        lib.yuma_shard_stage.argtypes = [i32, i32, vp, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp,
+                                         vp, sz, vp]
+        lib.yuma_shard_stage.restype = i32
         lib.yuma_synth_weights.argtypes = [ctypes.c_uint64, i32, i32, i32, i32, i32, vp, vp]
         lib.yuma_synth_weights.restype = i32
         lib.yuma_last_error.argtypes = []
@@ -312,6 +326,28 @@ def run(variant: int, params: list[YumaParamsC], W: torch.Tensor, S: torch.Tenso
     # keep inputs alive until the stream has consumed them
     keep["_inputs"] = (W, S, B_init, Wprev_init, prm, workspace)
     return RunResult(o["Dn"], o["C"], o["I"], o["B_final"], o.get("B_hist"), keep)
+
+
+def shard_stage(stage: int, variant: int, prm: torch.Tensor, W: torch.Tensor, S: torch.Tensor,
+                B_init: torch.Tensor | None, Wprev_init: torch.Tensor | None, *, M_total: int,
+                col0: int, io: dict, out: dict, workspace: torch.Tensor) -> None:
+    """One stage of a miner-column-sharded run (yuma_shard_stage). W [E,N,V,M]
+    holds this shard's columns; `io` maps SHARD_IO_FIELDS to device tensors;
+    `out` maps OUTPUT_FIELDS to device tensors (local columns)."""
+    lib = load_library()
+    E, N, V, M = W.shape
+    for k in io:
+        if k not in SHARD_IO_FIELDS:
+            raise KeyError(f"unknown shard io field {k}")
+    cio = YumaShardIOC(M_total=int(M_total), col0=int(col0),
+                       **{k: _ptr(io.get(k)) for k in SHARD_IO_FIELDS})
+    outs = YumaOutputsC(**{k: _ptr(out.get(k)) for k in OUTPUT_FIELDS})
+    stream = torch.cuda.current_stream(W.device).cuda_stream
+    _check(lib.yuma_shard_stage(stage, variant, prm.data_ptr(), N, E, V, M, W.data_ptr(),
+                                S.data_ptr(), _ptr(B_init), _ptr(Wprev_init),
+                                ctypes.addressof(cio), ctypes.addressof(outs),
+                                workspace.data_ptr(), workspace.numel(), stream),
+           f"yuma_shard_stage({stage})")
 
 
 def synth_weights(seed: int, E: int, N: int, V: int, M: int, t0: int = 0,
