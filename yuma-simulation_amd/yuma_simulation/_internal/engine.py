@@ -116,7 +116,7 @@ def load_library(path: str | None = None):
     with _lock:
         if _lib is not None:
             return _lib
-        p = path or LIB_PATH
+        p = path or os.environ.get("YUMA_LIB") or LIB_PATH  # YUMA_LIB: A/B builds (tools/ab_lib.sh)
         if not os.path.exists(p):
             raise EngineUnavailable(
                 f"{LIB_NAME} not found at {p}; build it with `python -c 'import __graft_entry__ as g; g.build()'`"
