@@ -11,6 +11,14 @@ dividends — the epoch-step contract of SURVEY §8d.
 Multi-GPU (torchrun, one process per GPU): scenario sharding — every rank runs
 its own subnet (its own seed), no data-path collective; weak scaling.
 
+Other BASELINE.json configs (`--config`, not what the driver runs):
+  c3  batched parameter sweep: 512 scenarios per GPU of 256 x 4096 over the
+      bond_alpha x kappa x liquid x (alpha_low, alpha_high) grid, Yuma 4;
+  c4  wide subnet 256 x 65536, miner columns sharded across the ranks
+      (RCCL all-gathers of per-shard partials between the engine's stages);
+  c5  the full dividend sheet (4 bond penalties x 14 cases x 9 versions =
+      504 runs) through generate_total_dividends_tables.
+
 Prints ONE JSON line (rank 0) with the driver's fields plus `roofline`
 (dominant kernel, algorithmic bytes / measured device time from HIP events)
 and `cpu_baseline` (the numpy oracle on a bounded sample, host cores).
@@ -103,34 +111,68 @@ def load_traffic(cfg: dict, dominant: str):
     return None if k is None else k.get("hbm_bytes_per_scenario_epoch")
 
 
-def main():
-    ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--epochs", type=int, default=1000)
-    ap.add_argument("--validators", type=int, default=256)
-    ap.add_argument("--miners", type=int, default=4096)
-    ap.add_argument("--scenarios", type=int, default=1, help="scenarios per GPU")
-    ap.add_argument("--version", default="Yuma 3 (Rhef)")
-    ap.add_argument("--liquid", action="store_true")
-    ap.add_argument("--no-history", action="store_true", help="do not write every epoch's bond state")
-    ap.add_argument("--chunk", type=int, default=0, help="epochs per phase-1 batch (0 = engine default)")
-    ap.add_argument("--seed", type=lambda s: int(s, 0), default=0x5EED0002)
-    ap.add_argument("--cpu-epochs", type=int, default=160)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--profile-reps", type=int, default=3)
-    args = ap.parse_args()
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = world > 1
+def timed(step, warmup: int, steps: int, dist: bool, dev) -> float:
+    """W untimed warmups, then K steps between barrier + synchronize; the
+    max over ranks of the elapsed wall time."""
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
     if dist:
         import torch.distributed as tdist
 
-        torch.cuda.set_device(local)
-        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        tdist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        tdist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed
+
+
+def base_line(args, world: int, value: float, unit: str, elapsed: float, scaling: str, config: dict) -> dict:
+    return {
+        "metric": METRIC,
+        "value": round(value, 1),
+        "unit": unit,
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": scaling,
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (integer-valued weights, stakes summing to 2^20; SURVEY \u00a78d generator)",
+        "config": config,
+    }
+
+
+SWEEP_BOND_ALPHA = [0.01 + (0.5 - 0.01) * i / 15 for i in range(16)]
+SWEEP_KAPPA = [0.3 + (0.7 - 0.3) * i / 15 for i in range(16)]
+SWEEP_ALPHAS = [(lo, hi) for lo in (0.6, 0.65, 0.7, 0.75) for hi in (0.9, 0.99)]
+
+
+def sweep_config(g: int):
+    """Scenario g of the c3 grid (SURVEY \u00a78d): 16 bond_alpha x 16 kappa x
+    2 liquid x 8 (alpha_low, alpha_high) = 4096 scenarios."""
+    from yuma_simulation._internal.yumas import SimulationHyperparameters, YumaConfig, YumaParams
+
+    lo, hi = SWEEP_ALPHAS[(g // 512) % 8]
+    return YumaConfig(simulation=SimulationHyperparameters(kappa=SWEEP_KAPPA[(g // 16) % 16]),
+                      yuma_params=YumaParams(bond_alpha=SWEEP_BOND_ALPHA[g % 16],
+                                             liquid_alpha=bool((g // 256) % 2),
+                                             alpha_low=lo, alpha_high=hi))
+
+
+def bench_engine(args, world: int, rank: int, dist: bool) -> dict:
+    """c2 (default) and c3: engine.run over E epochs of N scenarios per GPU."""
     from yuma_simulation._internal import engine, synth
     from yuma_simulation._internal.simulation_utils import resolve_version
     from yuma_simulation._internal.yumas import YumaConfig, YumaParams
@@ -138,9 +180,12 @@ def main():
     dev = engine.device()
     E, V, M, N = args.epochs, args.validators, args.miners, args.scenarios
     variant, _ = resolve_version(args.version)
-    cfg = YumaConfig(yuma_params=YumaParams(liquid_alpha=args.liquid))
-    params = [engine.make_params(variant, cfg) for _ in range(N)]
-    liquid = params[0].liquid_mode != engine.LIQUID_OFF
+    if args.config == "c3":
+        cfgs = [sweep_config(rank * N + i) for i in range(N)]
+    else:
+        cfgs = [YumaConfig(yuma_params=YumaParams(liquid_alpha=args.liquid))] * N
+    params = [engine.make_params(variant, c) for c in cfgs]
+    liquid = any(p.liquid_mode != engine.LIQUID_OFF for p in params)
     hist = not args.no_history
     seed = args.seed + 7919 * rank  # each rank simulates its own subnet(s)
 
@@ -157,26 +202,8 @@ def main():
     def step():
         return engine.run(variant, params, W, S, want_hist=hist, out=out, workspace=ws, chunk_epochs=chunk)
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if dist:
-        tdist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if dist:
-        tdist.barrier()
-    elapsed = time.perf_counter() - t0
-    if dist:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    ms_per_step = elapsed / args.steps * 1e3
-    total_units = float(E) * N * world * args.steps
-    value = total_units / elapsed
+    elapsed = timed(step, args.warmup, args.steps, dist, dev)
+    value = float(E) * N * world * args.steps / elapsed
 
     # per-phase device time from HIP events on the launch stream (separate,
     # untimed passes of the same step)
@@ -198,40 +225,192 @@ def main():
     dom_name = engine.PHASES[dom]
     dom_bytes = phase_bytes(dom_name, V, M, variant, liquid, hist, eff_chunk) * units
     achieved = dom_bytes / (phases[dom] * 1e-3) / 1e9
-    workload = {"workload": f"c2: single subnet {V}V x {M}M x {E} epochs, {args.version}"
-                            + (" liquid" if liquid else ""),
-                "V": V, "M": M, "epochs": E, "scenarios_per_gpu": N, "version": args.version,
-                "bond_history": hist, "parallelism": f"scenario-sharded x{world}" if world > 1 else "single GPU"}
+    if args.config == "c3":
+        wl = (f"c3: parameter sweep, {N} scenarios per GPU (of the 4096-point bond_alpha x kappa x "
+              f"liquid x alpha grid) of {V}V x {M}M x {E} epochs, {args.version}")
+    else:
+        wl = f"c2: single subnet {V}V x {M}M x {E} epochs, {args.version}" + (" liquid" if liquid else "")
+    workload = {"workload": wl, "V": V, "M": M, "epochs": E, "scenarios_per_gpu": N, "version": args.version,
+                "bond_history": hist,
+                "parallelism": f"scenario-sharded x{world}" if world > 1 else "single GPU"}
     traffic = load_traffic({k: workload[k] for k in ("V", "M", "epochs", "version", "bond_history")}, dom_name)
-
-    line = {
-        "metric": METRIC,
-        "value": round(value, 1),
-        "unit": "scenario-epochs/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(ms_per_step, 4),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "f32",
-        "data": "synthetic (integer-valued weights, stakes summing to 2^20; SURVEY §8d generator)",
-        "config": workload,
-        "roofline": {
-            "bound": "hbm",
-            "kernel": f"k_{dom_name}",
-            "achieved": round(achieved, 1),
-            "peak": HBM_PEAK_GBPS,
-            "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBPS, 4),
-            "traffic": traffic,
-        },
-        "contract_GBps": round(value / world * contract_bytes(V, M, variant) / 1e9, 1),
-        "phases": phase_info,
+    line = base_line(args, world, value, "scenario-epochs/s", elapsed, "weak", workload)
+    line["roofline"] = {
+        "bound": "hbm",
+        "kernel": f"k_{dom_name}",
+        "achieved": round(achieved, 1),
+        "peak": HBM_PEAK_GBPS,
+        "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBPS, 4),
+        "traffic": traffic,
     }
+    line["contract_GBps"] = round(value / world * contract_bytes(V, M, variant) / 1e9, 1)
+    line["phases"] = phase_info
     if rank == 0 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(args.version, V, M, args.cpu_epochs, 16, args.seed)
+        if args.config == "c3":
+            line["cpu_baseline"] = cpu_baseline_c3(args.version, V, M, args.seed)
+        else:
+            line["cpu_baseline"] = cpu_baseline(args.version, V, M, args.cpu_epochs, 16, args.seed)
+    return line
+
+
+def cpu_baseline_c3(version: str, V: int, M: int, seed: int) -> dict:
+    """Oracle on 8 scenarios x 16 epochs of the c3 sweep (one host core)."""
+    from oracle import yuma_oracle as orc
+    from yuma_simulation._internal import synth
+
+    n_s, E = 8, 16
+    W = synth.weights(seed, E, n_s, V, M)
+    S = synth.stakes(seed, E, n_s, V)
+    t0 = time.perf_counter()
+    for i in range(n_s):
+        orc.run(version, W[:, i], S[:, i], sweep_config(i * 257))
+    dt = time.perf_counter() - t0
+    return {"value": round(n_s * E / dt, 3), "unit": "scenario-epochs/s", "cores": 1, "kind": "port",
+            "sample": f"{n_s} sweep scenarios x {E} epochs of {version} at {V}x{M}, numpy oracle, 1 thread, "
+                      f"{dt:.1f} s"}
+
+
+def bench_wide(args, world: int, rank: int, dist: bool) -> dict:
+    """c4: one wide subnet, miner columns sharded across the ranks."""
+    from yuma_simulation._internal import engine, synth, wide
+    from yuma_simulation._internal.simulation_utils import resolve_version
+    from yuma_simulation._internal.yumas import YumaConfig
+
+    dev = engine.device()
+    E, V, M = args.epochs, args.validators, args.miners
+    variant, _ = resolve_version(args.version)
+    params = [engine.make_params(variant, YumaConfig())]
+    cols = wide.column_ranges(M, world)[rank]
+    W = engine.synth_weights(args.seed, E, 1, V, M)[..., cols.start:cols.stop].contiguous()
+    torch.cuda.empty_cache()
+    S = torch.from_numpy(synth.stakes(args.seed, E, 1, V)).to(dev)
+    hist = not args.no_history
+    if dist:
+        def step():
+            return wide.run_wide_distributed(variant, params, W, S, M_total=M, want_hist=hist)
+    else:
+        def step():
+            return wide.run_wide_local(variant, params, W, S, 1, want_hist=hist)
+
+    elapsed = timed(step, args.warmup, args.steps, dist, dev)
+    value = float(E) * args.steps / elapsed  # one subnet: total work fixed
+    per_gpu_bytes = contract_bytes(V, len(cols), variant) * E * args.steps / elapsed / 1e9
+    workload = {"workload": f"c4: wide subnet {V}V x {M}M x {E} epochs, {args.version}, miner columns "
+                            f"sharded x{world}", "V": V, "M": M, "epochs": E, "scenarios_per_gpu": 1,
+                "version": args.version, "bond_history": hist,
+                "parallelism": f"miner-column sharded x{world} (all-gather of per-shard partials)"}
+    line = base_line(args, world, value, "scenario-epochs/s", elapsed, "strong", workload)
+    line["roofline"] = {"bound": "hbm", "kernel": "whole epoch step (all stages; contract bytes / wall time)",
+                        "achieved": round(per_gpu_bytes, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                        "frac": round(per_gpu_bytes / HBM_PEAK_GBPS, 4), "traffic": None}
+    if rank == 0 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(args.version, V, M, 3, 3, args.seed)
+    return line
+
+
+def bench_sheet(args, world: int, rank: int, dist: bool) -> dict:
+    """c5: the dividend sheet of all four bond penalties (504 runs)."""
+    from yuma_simulation._internal import engine
+    from yuma_simulation._internal.cases import cases
+    from yuma_simulation._internal.simulation_utils import (
+        SHEET_BOND_PENALTIES,
+        _sheet_runs,
+        generate_total_dividends_tables,
+        run_simulations,
+        sheet_yuma_versions,
+    )
+    from yuma_simulation._internal.yumas import SimulationHyperparameters
+
+    dev = engine.device()
+    hypers = [SimulationHyperparameters(bond_penalty=b) for b in SHEET_BOND_PENALTIES]
+    versions = sheet_yuma_versions()
+    runs = [r for h in hypers for r in _sheet_runs(cases, versions, h)]
+    units = sum(r.case.num_epochs for r in runs)
+    if dist:
+        mine = runs[rank::world]
+
+        def step():
+            return run_simulations(mine, want_bonds=False, want_incentives=False)
+    else:
+        def step():
+            return generate_total_dividends_tables(cases, versions, hypers)
+
+    elapsed = timed(step, args.warmup, args.steps, dist, dev)
+    value = units * args.steps / elapsed
+    workload = {"workload": f"c5: dividend sheet, {len(runs)} runs (4 bond penalties x {len(cases)} cases x "
+                            f"{len(versions)} versions), {units} scenario-epochs", "runs": len(runs),
+                "scenario_epochs": units, "parallelism": f"runs sharded x{world}" if world > 1 else "single GPU"}
+    line = base_line(args, world, value, "scenario-epochs/s", elapsed, "strong", workload)
+    line["data"] = "the reference's built-in cases (cases.py)"
+    line["roofline"] = {"bound": "latency", "kernel": "whole sheet (3x2 matrices: launch/host bound)",
+                        "achieved": None, "peak": None, "unit": None, "frac": None, "traffic": None}
+    if rank == 0 and not args.no_cpu_baseline:
+        from oracle import yuma_oracle as orc
+
+        t0 = time.perf_counter()
+        for r in runs:
+            W = torch.stack(list(r.case.weights_epochs)[: r.case.num_epochs]).numpy()
+            S = torch.stack(list(r.case.stakes_epochs)[: r.case.num_epochs]).numpy()
+            orc.run(r.yuma_version, W, S, r.yuma_config, r.case.reset_bonds_epoch, r.case.reset_bonds_index,
+                    validators=r.case.validators)
+        dt = time.perf_counter() - t0
+        line["cpu_baseline"] = {"value": round(units / dt, 1), "unit": "scenario-epochs/s", "cores": 1,
+                                "kind": "port", "sample": f"all {len(runs)} sheet runs, numpy oracle, 1 thread, "
+                                                          f"{dt:.1f} s"}
+    return line
+
+
+DEFAULTS = {  # per config: epochs, validators, miners, scenarios per GPU, version, history
+    "c2": (1000, 256, 4096, 1, "Yuma 3 (Rhef)", True),
+    "c3": (32, 256, 4096, 512, "Yuma 4 (Rhef+relative bonds)", False),
+    "c4": (100, 256, 65536, 1, "Yuma 3 (Rhef)", False),
+    "c5": (40, 3, 2, 1, "", False),
+}
+
+
+def main():
+    ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", choices=sorted(DEFAULTS), default="c2",
+                    help="BASELINE.json workload (c2 is the headline metric)")
+    ap.add_argument("--epochs", type=int, default=None)
+    ap.add_argument("--validators", type=int, default=None)
+    ap.add_argument("--miners", type=int, default=None)
+    ap.add_argument("--scenarios", type=int, default=None, help="scenarios per GPU")
+    ap.add_argument("--version", default=None)
+    ap.add_argument("--liquid", action="store_true")
+    ap.add_argument("--no-history", action="store_true", help="do not write every epoch's bond state")
+    ap.add_argument("--chunk", type=int, default=0, help="epochs per phase-1 batch (0 = engine default)")
+    ap.add_argument("--seed", type=lambda s: int(s, 0), default=None)
+    ap.add_argument("--cpu-epochs", type=int, default=400)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--profile-reps", type=int, default=3)
+    args = ap.parse_args()
+    E, V, M, N, version, hist = DEFAULTS[args.config]
+    args.epochs = args.epochs or E
+    args.validators = args.validators or V
+    args.miners = args.miners or M
+    args.scenarios = args.scenarios or N
+    args.version = args.version or version
+    if not hist:
+        args.no_history = True
+    if args.seed is None:
+        args.seed = {"c3": 0x5EED0003, "c4": 0x5EED0004}.get(args.config, 0x5EED0002)
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = world > 1
+    if dist:
+        import torch.distributed as tdist
+
+        torch.cuda.set_device(local)
+        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    run = {"c2": bench_engine, "c3": bench_engine, "c4": bench_wide, "c5": bench_sheet}[args.config]
+    line = run(args, world, rank, dist)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist:

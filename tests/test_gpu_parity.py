@@ -77,6 +77,34 @@ def test_sheet_csv_byte_identical(bi):
     assert hashlib.md5(buf.getvalue().encode()).hexdigest() == meta["csv_md5"][name]
 
 
+def test_sheet_all_tables_batched_and_scripts(tmp_path):
+    """All four sheets from ONE batched call (generate_total_dividends_tables,
+    config c5) and the scripts/ generator: the reference's CSV bytes."""
+    import sys
+
+    from yuma_simulation._internal.simulation_utils import (
+        SHEET_BOND_PENALTIES,
+        generate_total_dividends_tables,
+        sheet_yuma_versions,
+    )
+
+    with open(os.path.join(GOLDEN, "sheet.json")) as f:
+        meta = json.load(f)
+    frames = generate_total_dividends_tables(
+        cases, sheet_yuma_versions(), [Y.SimulationHyperparameters(bond_penalty=b) for b in SHEET_BOND_PENALTIES])
+    for beta, df in zip(SHEET_BOND_PENALTIES, frames):
+        buf = io.StringIO()
+        df.to_csv(buf, index=False, float_format="%.6f")
+        assert buf.getvalue() == meta["csv"][f"total_dividends_b{beta}.csv"]
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    from scripts import total_dividends_sheet_generator as gen
+
+    for path in gen.main(str(tmp_path)):
+        with open(path, "rb") as f:
+            assert hashlib.md5(f.read()).hexdigest() == meta["csv_md5"][os.path.basename(path)]
+
+
 def test_sheet_runs_per_epoch(golden):
     """Every (beta, case, version) run: consensus exact, dividends / bonds /
     incentives within tolerance; all 504 runs go through batched launches."""

@@ -145,3 +145,30 @@ def test_synth_exactness_properties():
     # deterministic and scenario-distinct
     assert np.array_equal(W, synth.weights(5, 2, 2, 64, 4096))
     assert not np.array_equal(W[:, 0], W[:, 1])
+
+
+def test_sheet_versions_match_reference_scripts():
+    """sheet_yuma_versions() is the list both reference scripts sweep
+    (scripts/total_dividends_sheet_generator.py:25-48), as captured in specs."""
+    from dataclasses import asdict
+
+    from golden import specs
+    from yuma_simulation._internal.simulation_utils import SHEET_BOND_PENALTIES, sheet_yuma_versions
+    from yuma_simulation._internal.yumas import YumaParams
+
+    got = sheet_yuma_versions()
+    assert [v for v, _ in got] == specs.VERSIONS
+    assert list(SHEET_BOND_PENALTIES) == specs.BETAS
+    for (_, params), over in zip(got, specs.SHEET_PARAMS):
+        assert asdict(params) == asdict(YumaParams(**over))
+
+
+def test_scripts_import_without_gpu():
+    import importlib
+    import os
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    for name in ("scripts.total_dividends_sheet_generator", "scripts.charts_table_generator"):
+        assert callable(importlib.import_module(name).main)

@@ -130,26 +130,47 @@ def run_simulation(
     return run_simulations([SimulationRun(case, yuma_version, yuma_config)])[0]
 
 
-def generate_total_dividends_table(
-    cases: list[BaseCase],
-    yuma_versions: list[tuple[str, YumaParams]],
-    simulation_hyperparameters: SimulationHyperparameters,
-) -> pd.DataFrame:
-    """Total dividends per standardized validator and version (reference
-    simulation_utils.py:319-381). All (case, version) runs are batched."""
-    standardized = ["Validator A", "Validator B", "Validator C"]
+SHEET_BOND_PENALTIES = (0, 0.5, 0.99, 1.0)  # scripts/total_dividends_sheet_generator.py:14
+
+
+def sheet_yuma_versions() -> list[tuple[str, YumaParams]]:
+    """The nine (version, YumaParams) pairs both reference scripts sweep
+    (scripts/total_dividends_sheet_generator.py:25-48,
+    scripts/charts_table_generator.py:27-47)."""
+    from dataclasses import replace
+
+    base = YumaParams()
+    liquid = YumaParams(liquid_alpha=True)
+    y4_liquid = replace(YumaParams(bond_alpha=0.025, alpha_high=0.99, alpha_low=0.9), liquid_alpha=True)
+    n = _NAMES
+    return [
+        (n.YUMA_RUST, base), (n.YUMA, base), (n.YUMA_LIQUID, liquid), (n.YUMA2, base),
+        (n.YUMA3, base), (n.YUMA31, base), (n.YUMA32, base), (n.YUMA4, base),
+        (n.YUMA4_LIQUID, y4_liquid),
+    ]
+
+
+_STANDARDIZED = ["Validator A", "Validator B", "Validator C"]
+
+
+def _sheet_runs(cases: list[BaseCase], yuma_versions, hyper: SimulationHyperparameters):
     for case in cases:
         if len(case.validators) != 3:
             raise ValueError(f"Case '{case.name}' does not have exactly 3 validators.")
-    runs = [
-        SimulationRun(case, version, YumaConfig(simulation=simulation_hyperparameters, yuma_params=params))
+    return [
+        SimulationRun(case, version, YumaConfig(simulation=hyper, yuma_params=params))
         for case in cases
         for version, params in yuma_versions
     ]
-    results = iter(run_simulations(runs, want_bonds=False, want_incentives=False))
+
+
+def _sheet_frame(cases: list[BaseCase], yuma_versions, results) -> pd.DataFrame:
+    """Rows of the dividend sheet from the runs' results, in _sheet_runs order
+    (reference simulation_utils.py:341-381)."""
+    results = iter(results)
     rows: list[dict[str, object]] = []
     for case in cases:
-        mapping = dict(zip(case.validators, standardized))
+        mapping = dict(zip(case.validators, _STANDARDIZED))
         row: dict[str, object] = {"Case": case.name}
         for version, _ in yuma_versions:
             dividends, _, _ = next(results)
@@ -160,15 +181,44 @@ def generate_total_dividends_table(
                 num_epochs=case.num_epochs,
             )
             by_std = {mapping[v]: totals.get(v, 0.0) for v in case.validators}
-            for std in standardized:
+            for std in _STANDARDIZED:
                 row[f"{std} - {version}"] = by_std.get(std, 0.0)
         rows.append(row)
     df = pd.DataFrame(rows)
     columns = ["Case"] + [
-        f"{std} - {version}" for version, _ in yuma_versions for std in standardized
+        f"{std} - {version}" for version, _ in yuma_versions for std in _STANDARDIZED
         if f"{std} - {version}" in df.columns
     ]
     return df[columns]
+
+
+def generate_total_dividends_table(
+    cases: list[BaseCase],
+    yuma_versions: list[tuple[str, YumaParams]],
+    simulation_hyperparameters: SimulationHyperparameters,
+) -> pd.DataFrame:
+    """Total dividends per standardized validator and version (reference
+    simulation_utils.py:319-381). All (case, version) runs are batched."""
+    runs = _sheet_runs(cases, yuma_versions, simulation_hyperparameters)
+    return _sheet_frame(cases, yuma_versions, run_simulations(runs, want_bonds=False, want_incentives=False))
+
+
+def generate_total_dividends_tables(
+    cases: list[BaseCase],
+    yuma_versions: list[tuple[str, YumaParams]],
+    simulation_hyperparameters: list[SimulationHyperparameters],
+) -> list[pd.DataFrame]:
+    """One dividend table per hyperparameter set (the sheet script's four
+    bond penalties, scripts/total_dividends_sheet_generator.py:14-59), with the
+    runs of ALL tables packed into one engine call per variant (config c5:
+    504 runs in five launches sequences instead of twenty)."""
+    per = [_sheet_runs(cases, yuma_versions, h) for h in simulation_hyperparameters]
+    flat = run_simulations([r for runs in per for r in runs], want_bonds=False, want_incentives=False)
+    out, k = [], 0
+    for runs in per:
+        out.append(_sheet_frame(cases, yuma_versions, flat[k:k + len(runs)]))
+        k += len(runs)
+    return out
 
 
 from yuma_simulation._internal.html_tables import (  # noqa: E402,F401  (re-exported surface)
