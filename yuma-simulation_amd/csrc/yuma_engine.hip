@@ -39,6 +39,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <mutex>
 #include <vector>
 
 #include "yuma_hip.h"
@@ -2518,6 +2519,63 @@ struct PhaseTimer {
   }
 };
 
+// Second in-order stream for the chunk pipeline (one per device, created on
+// first use, never destroyed: it lives as long as the process).
+hipStream_t aux_stream() {
+  static std::mutex mu;
+  static hipStream_t streams[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  std::lock_guard<std::mutex> g(mu);
+  if (streams[dev] == nullptr &&
+      hipStreamCreateWithFlags(&streams[dev], hipStreamNonBlocking) != hipSuccess)
+    streams[dev] = nullptr;
+  return streams[dev];
+}
+// st2 waits for everything enqueued on st1 so far (an event edge: also valid
+// inside hipStreamBeginCapture, where it becomes a graph dependency). The
+// events come from a recycled per-device pool: a wait binds to the record
+// that precedes it, so re-recording an event later does not disturb it, and
+// no event is destroyed while work is pending.
+bool stream_edge(hipStream_t st1, hipStream_t st2) {
+  constexpr int kPool = 256;
+  static std::mutex mu;
+  static hipEvent_t pool[64][kPool] = {};
+  static unsigned next[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return false;
+  hipEvent_t e;
+  {
+    std::lock_guard<std::mutex> g(mu);
+    hipEvent_t& slot = pool[dev][next[dev]++ % kPool];
+    if (slot == nullptr && hipEventCreateWithFlags(&slot, hipEventDisableTiming) != hipSuccess) {
+      slot = nullptr;
+      return false;
+    }
+    e = slot;
+  }
+  return hipEventRecord(e, st1) == hipSuccess && hipStreamWaitEvent(st2, e, 0) == hipSuccess;
+}
+// Chunk pipeline (opt-in: YUMA_PIPE=k runs k chunks): phase 1a-1c (row sums,
+// consensus, quantisation) of chunk k+1 run on the caller's stream while
+// chunk k's rank, incentive, bond scan and finalize run on the auxiliary
+// stream, to overlap the VALU-bound consensus with the HBM-bound bond scan.
+// Measured slower on MI355X at c2 (5.21 ms at 8 chunks, 5.12 at 4, 5.50 at
+// 16 vs 4.99 unpipelined), so one chunk, one stream by default.
+int pipe_chunks(int E) {
+  static int knob = -2;
+  if (knob == -2) {
+    const char* e = getenv("YUMA_PIPE");
+    knob = e ? atoi(e) : 0;
+  }
+  if (knob <= 0) return 1;
+  const int want = knob;
+  const int minc = 32;  // epochs per chunk below which the bond scan's fill dominates
+  int n = E / minc;
+  if (n > want) n = want;
+  return n < 1 ? 1 : n;
+}
+
 int run_impl(int variant, const yuma_params_t* prm, int N, int E, int V, int M, const float* W,
              const float* S, const float* B_init, const float* Wprev_init,
              const yuma_outputs_t* out, void* workspace, size_t ws_bytes, int chunk,
@@ -2557,10 +2615,11 @@ int run_impl(int variant, const yuma_params_t* prm, int N, int E, int V, int M, 
   float* ba_buf = out->bond_alpha ? out->bond_alpha : ws.ba;
 
   if (chunk <= 0 || chunk > E) {
-    // one chunk: streaming re-reads gain only ~10% from the 256 MB MALL on
-    // MI355X (tools/membw: 6.6-7.1 TB/s at 64-256 MB vs 6.44 TB/s from HBM),
-    // less than the per-launch cost of more chunks
-    chunk = E;
+    // caching a chunk in the 256 MB MALL gains only ~10% on MI355X
+    // (tools/membw: 6.6-7.1 TB/s at 64-256 MB vs 6.44 TB/s from HBM); chunks
+    // exist for the two-stream pipeline (pipe_chunks), not for reuse
+    const int nc = phase_ms != nullptr ? 1 : pipe_chunks(E);
+    chunk = (E + nc - 1) / nc;
   }
   (void)slice_elems;
 
@@ -2579,6 +2638,13 @@ int run_impl(int variant, const yuma_params_t* prm, int N, int E, int V, int M, 
   PhaseTimer tm{};
   tm.ms = phase_ms;
   tm.st = st;
+  // st runs phase 1a-1c; sb runs rank .. finalize (the same stream unless
+  // pipelined, see pipe_chunks)
+  hipStream_t sb = st;
+  if (phase_ms == nullptr && chunk < E && !fused) {
+    hipStream_t aux = aux_stream();
+    if (aux != nullptr && stream_edge(st, aux)) sb = aux;
+  }
 
   for (int c0 = 0, ci = 0; c0 < E; c0 += chunk, ++ci) {
     const int c1 = c0 + chunk < E ? c0 + chunk : E;
@@ -2645,17 +2711,18 @@ int run_impl(int variant, const yuma_params_t* prm, int N, int E, int V, int M, 
     tm.mark(2);
     YK_LAUNCH(yk::k_quantise<256>, ns, 256, st, ws.craw, prm, variant, N, M, s0, C, ws.qlev,
               ba_buf, ws.scal, nullptr, nullptr, 0);
+    if (sb != st && !stream_edge(st, sb)) return fail(YUMA_EHIP, "stream edge failed");
     tm.mark(3);
     if (vec)
-      launch_rank<true>(rc, ns * tiles, st, W, ws.rsd, ws.sn, C, Wprev_init,
+      launch_rank<true>(rc, ns * tiles, sb, W, ws.rsd, ws.sn, C, Wprev_init,
                         variant == YUMA_VARIANT_YUMA2, N, V, M, s0, tiles, out->R ? out->R : ws.R,
                         ws.rpart, out->Wn, out->Wc, ws.tvc, ws.tvn);
     else
-      launch_rank<false>(rc, ns * tiles, st, W, ws.rsd, ws.sn, C, Wprev_init,
+      launch_rank<false>(rc, ns * tiles, sb, W, ws.rsd, ws.sn, C, Wprev_init,
                          variant == YUMA_VARIANT_YUMA2, N, V, M, s0, tiles,
                          out->R ? out->R : ws.R, ws.rpart, out->Wn, out->Wc, ws.tvc, ws.tvn);
     tm.mark(4);
-    YK_LAUNCH(yk::k_incentive, ns, 256, st, out->R ? out->R : ws.R, ws.rpart, out->P, M, s0,
+    YK_LAUNCH(yk::k_incentive, ns, 256, sb, out->R ? out->R : ws.R, ws.rpart, out->P, M, s0,
               tiles, I, out->P ? out->T : nullptr, ws.scal, nullptr);
     }
 
@@ -2684,21 +2751,23 @@ int run_impl(int variant, const yuma_params_t* prm, int N, int E, int V, int M, 
     const long long nb = (long long)N * tiles * rowblocks;
     tm.mark(5);
     if (vec)
-      launch_bonds<true>(variant, rc, elemR, nb, st, A);
+      launch_bonds<true>(variant, rc, elemR, nb, sb, A);
     else
-      launch_bonds<false>(variant, rc, elemR, nb, st, A);
+      launch_bonds<false>(variant, rc, elemR, nb, sb, A);
     tm.mark(6);
-    YK_LAUNCH(yk::k_finalize, ns, 256, st, ws.dpart, ws.sn, variant, V, s0, tiles, ws.tvc,
+    YK_LAUNCH(yk::k_finalize, ns, 256, sb, ws.dpart, ws.sn, variant, V, s0, tiles, ws.tvc,
               ws.tvn, out->Dn, out->D, out->Tv);
     if (out->Sn != nullptr)
       (void)hipMemcpyAsync(out->Sn + s0 * V, ws.sn + s0 * V, (size_t)ns * V * 4,
-                           hipMemcpyDeviceToDevice, st);
+                           hipMemcpyDeviceToDevice, sb);
     if (out->alpha_ab != nullptr)
       (void)hipMemcpy2DAsync(out->alpha_ab + s0 * 2, 2 * sizeof(float), ws.scal + s0 * 8 + 1,
                              8 * sizeof(float), 2 * sizeof(float), (size_t)ns,
-                             hipMemcpyDeviceToDevice, st);
+                             hipMemcpyDeviceToDevice, sb);
     tm.mark(-1);  // end of chunk
   }
+  // join: the caller's stream sees every output
+  if (sb != st && !stream_edge(sb, st)) return fail(YUMA_EHIP, "stream join failed");
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(YUMA_EHIP, "HIP launch failed: %s", hipGetErrorString(e));
   if (phase_ms != nullptr) {
