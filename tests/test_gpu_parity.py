@@ -381,3 +381,40 @@ def test_deterministic_repeat():
     b = engine.run(engine.VARIANT_YUMA3, prm, W, S, want_hist=True)
     torch.cuda.synchronize()
     assert torch.equal(a.B_hist, b.B_hist) and torch.equal(a.Dn, b.Dn)
+
+
+@pytest.mark.parametrize("V,M", [(256, 4096), (64, 1000), (33, 65), (200, 260), (256, 64)])
+def test_rank_folded_into_bond_scan_matches_separate_pass(V, M, monkeypatch):
+    """k_bonds_rank (rank column sums inside the Yuma3/4 bond scan, dividends
+    as (sum_m B R) / R.sum()) against the separate rank pass (YUMA_RANKFUSE=0)
+    on the same inputs: consensus and bonds bitwise equal (the bond update is
+    the same arithmetic), rank, incentive and dividends within the north-star
+    1e-5 relative tolerance; and both against the oracle."""
+    E = 9
+    W = synth.weights(0x5EED0F, E, 2, V, M)
+    S = synth.stakes(0x5EED0F, E, 2, V, period=4)
+    cases_ = [("yuma3", "Yuma 3 (Rhef)", {}), ("yuma4", "Yuma 4 (Rhef+relative bonds)", {}),
+              ("yuma4", "Yuma 4 (Rhef+relative bonds) - liquid alpha on", {"liquid_alpha": True})]
+    for variant, version, extra in cases_:
+        vid = VARIANT_ID[variant]
+        cfgs = [config_from(dict(extra, kappa=0.5)), config_from(dict(extra, kappa=0.4))]
+        prm = [engine.make_params(vid, c) for c in cfgs]
+        for k, p in enumerate(prm):  # one scenario with a conditional bond reset
+            if k == 1:
+                p.reset_mode, p.reset_epoch, p.reset_index = engine.RESET_IF_ZERO_CONSENSUS, 4, 3
+        Wt, St = torch.from_numpy(W), torch.from_numpy(S)
+        monkeypatch.setenv("YUMA_RANKFUSE", "1")
+        a = engine.run(vid, prm, Wt, St, want_hist=True, want=("R", "D"), chunk_epochs=4)
+        monkeypatch.setenv("YUMA_RANKFUSE", "0")
+        b = engine.run(vid, prm, Wt, St, want_hist=True, want=("R", "D"))
+        torch.cuda.synchronize()
+        tag = f"{variant} {version} {V}x{M}"
+        assert torch.equal(a.C, b.C), tag
+        assert torch.equal(a.B_hist, b.B_hist), tag
+        for name, x, y in (("R", a.extra["R"], b.extra["R"]), ("I", a.I, b.I), ("D", a.extra["D"], b.extra["D"]),
+                           ("Dn", a.Dn, b.Dn)):
+            assert_close(x.cpu().numpy(), y.cpu().numpy(), what=f"{tag} {name}")
+        ref = orc.run(version, W[:, 0], S[:, 0], cfgs[0])
+        np.testing.assert_array_equal(a.C[:, 0].cpu().numpy(), ref["C"])
+        assert_close(a.Dn[:, 0].cpu().numpy(), ref["Dn"], what=f"{tag} Dn vs oracle")
+        assert_close(a.I[:, 0].cpu().numpy(), ref["I"], what=f"{tag} I vs oracle")

@@ -1633,6 +1633,8 @@ struct BondArgs {
   float* Wb_out;
   float* Binst_out;
   float* dpart;
+  float* R;      // k_bonds_rank: server_rank [slice][M]
+  float* rpart;  // k_bonds_rank: per-strip rank sums [slice][tiles]
   int N, V, M, tiles, rowblocks, t0, t1;
 };
 
@@ -1904,8 +1906,10 @@ __global__ __launch_bounds__(NT) void k_bonds(BondArgs A) {
 // (a register ring refilled as each epoch is consumed), so the per-epoch HBM
 // latency is hidden behind P-1 epochs of work.
 // ---------------------------------------------------------------------------
-template <int VARIANT, int R, bool VEC, int P, bool NTS, bool VECI = false>
-__global__ __launch_bounds__(256) void k_bonds_elem(BondArgs A) {
+// WPE: minimum waves per SIMD the register allocation must allow (0 = free)
+template <int VARIANT, int R, bool VEC, int P, bool NTS, bool VECI = false, int WPE = 0>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? WPE : 1)))
+void k_bonds_elem(BondArgs A) {
   constexpr int G = 16;
   const Lay L = lay();
   const int tile = blockIdx.x % A.tiles;
@@ -1930,14 +1934,25 @@ __global__ __launch_bounds__(256) void k_bonds_elem(BondArgs A) {
     has_old = src != nullptr;
 #pragma unroll
     for (int i = 0; i < R; ++i) {
-      const int row = row0 + G * i;
-      if (has_old && row < V)
-        load4<VEC>(src + n * VM + (long long)row * M, m, M, B[i]);
+      if (has_old)
+        load4c<VEC>(src + n * VM, row0 + G * i, V, m, M, B[i]);
       else
 #pragma unroll
         for (int c = 0; c < 4; ++c) B[i][c] = 0.0f;
     }
   }
+  // The reset test (the previous epoch's consensus of one miner) is known
+  // before the scan: read it here, not inside the ring loop.
+  bool reset_fire = false;
+  if (reset_mode != YUMA_RESET_NONE && reset_epoch >= A.t0 && reset_epoch < A.t1 &&
+      reset_index >= 0 && reset_index < M) {
+    reset_fire = reset_mode == YUMA_RESET_ALWAYS;
+    if (reset_mode == YUMA_RESET_IF_ZERO_CONSENSUS && reset_epoch >= 1)
+      reset_fire = A.C[((long long)(reset_epoch - 1) * N + n) * M + reset_index] == 0.0f;
+  }
+  // retire these loads before the ring fills (vmcnt(0), an s_waitcnt the
+  // compiler's waitcnt pass sees), or their scores survive the loop back-edge
+  __builtin_amdgcn_s_waitcnt(0x0F70);
 
   float rw[P][R][4], rd[P][R], rsn[P][R], ri[P][4], rba[P][4];
   auto fetch = [&](int k, int t) {
@@ -1958,28 +1973,21 @@ __global__ __launch_bounds__(256) void k_bonds_elem(BondArgs A) {
       if (liquid) vec4raw(A.ba + slice * M, m, M, rba[k]);
     }
   };
+  // Every ring load is unconditional (epochs past the end re-read the last
+  // one) and the main loop runs whole ring turns only: a load on some paths
+  // into the loop header makes the waitcnt pass assume the shortest history
+  // and wait vmcnt(0) every epoch, i.e. drain the ring.
 #pragma unroll
-  for (int k = 0; k < P; ++k)
-    if (A.t0 + k < A.t1) fetch(k, A.t0 + k);
+  for (int k = 0; k < P; ++k) fetch(k, min(A.t0 + k, A.t1 - 1));
 
-  for (int tb = A.t0; tb < A.t1; tb += P) {
-#pragma unroll
-    for (int k = 0; k < P; ++k) {
-      const int t = tb + k;
-      if (t >= A.t1) break;
+  auto step = [&](int k, int t) {
       const long long slice = (long long)t * N + n;
-      if (has_old && reset_mode != YUMA_RESET_NONE && t == reset_epoch && reset_index >= 0 &&
-          reset_index < M) {
-        bool fire = reset_mode == YUMA_RESET_ALWAYS;
-        if (reset_mode == YUMA_RESET_IF_ZERO_CONSENSUS && t >= 1)
-          fire = A.C[(slice - N) * M + reset_index] == 0.0f;
+      if (has_old && reset_fire && t == reset_epoch) {
         const int c = reset_index - m;
-        if (fire && c >= 0 && c < 4)
 #pragma unroll
-          for (int i = 0; i < R; ++i)
+        for (int i = 0; i < R; ++i)
 #pragma unroll
-            for (int cc = 0; cc < 4; ++cc)
-              if (cc == c) B[i][cc] = 0.0f;
+          for (int cc = 0; cc < 4; ++cc) B[i][cc] = (cc == c) ? 0.0f : B[i][cc];
       }
       float bac[4], omba[4];
 #pragma unroll
@@ -2037,14 +2045,247 @@ __global__ __launch_bounds__(256) void k_bonds_elem(BondArgs A) {
         if (L.c4 == 0 && row < V) A.dpart[(slice * A.tiles + tile) * V + row] = d;
       }
       has_old = true;
-      if (t + P < A.t1) fetch(k, t + P);
+  };
+  int tb = A.t0;
+  for (; tb + P <= A.t1; tb += P) {
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+      step(k, tb + k);
+      fetch(k, min(tb + k + P, A.t1 - 1));
     }
   }
+#pragma unroll
+  for (int k = 0; k < P; ++k)  // the last partial turn: inputs already in the ring
+    if (tb + k < A.t1) step(k, tb + k);
 #pragma unroll
   for (int i = 0; i < R; ++i) {
     const int row = row0 + G * i;
     if (row < V) store4<VEC>(A.Bstate + n * VM + (long long)row * M, m, M, B[i]);
   }
+}
+
+// ---------------------------------------------------------------------------
+// Phase 2 with the rank folded in (Yuma3 yumas.py:439-475, Yuma4 :533-590;
+// run outputs only, V <= 256). A block owns every validator row of a
+// 16-miner column strip (thread = 1 row x 4 miners, 16 rows per wave), so the
+// rank column sum R[m] = sum_v S W_clipped (yumas.py:442) is a block-local
+// reduction over the W tile the bond update already holds in registers, and
+// the separate rank pass (a whole extra read of W) disappears.
+//   D needs I = R / R.sum() (yumas.py:445), and R.sum() spans every strip, so
+// the strip accumulates sum_m B[v,m] R[m] instead and k_finalize divides by
+// R.sum() once (sum_m B I = (sum_m B R) / R.sum(), the same quantity up to
+// fp32 rounding of the reassociation; the 1e-5 tolerance of the north star).
+//   Epochs go in groups of P (the prefetch ring depth): each epoch's partials
+// S*min(W, C) go to LDS ([epoch][miner][row], padded), then per group one
+// barrier, a fixed-order reduction (wave w takes (epoch, miner) pairs w,
+// w + nw, ...: rows lane + 64j sequentially, then the 64-lane butterfly), a
+// second barrier, and the group's dividend partials from the bond states kept
+// in registers. Two barriers per P epochs keep the waves loosely coupled; the
+// prefetch ring stays in flight across them (no vmcnt drain at a barrier).
+// ---------------------------------------------------------------------------
+// torch.minimum / torch.maximum in one instruction (gfx950 v_minimum3_f32 /
+// v_maximum3_f32, NaN-propagating); unlike tmin/tmax they order -0 < +0,
+// which no sum, product or comparison downstream can tell apart
+__device__ __forceinline__ float vmin(float a, float b) { return __builtin_elementwise_minimum(a, b); }
+__device__ __forceinline__ float vmax(float a, float b) { return __builtin_elementwise_maximum(a, b); }
+
+constexpr int kRankTileM = 16;  // miners per column strip
+constexpr int kRankLdsV = 260;  // padded row stride of the partial tile (banks)
+constexpr int kRankP = 4;       // prefetch depth (epochs in flight)
+
+// G: epochs per group (barrier pair), a multiple of the ring depth P
+template <int VARIANT, bool VEC, int P, int G>
+__global__ __launch_bounds__(1024) void k_bonds_rank(BondArgs A) {
+  static_assert(G % P == 0, "group = whole ring turns");
+  __shared__ float part[G][kRankTileM][kRankLdsV];
+  __shared__ __align__(16) float rsh[G][kRankTileM];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int q = lane & 3;
+  const int row = wave * 16 + (lane >> 2);
+  // XCD-aware order: blocks b and b + 8 share an XCD (round-robin dispatch),
+  // so give each XCD a contiguous run of strips. A 16-miner strip row is half
+  // a 128-B line; its neighbour strip then sits in the same L2, and the two
+  // halves of every W line / bond-history line meet there instead of being
+  // fetched (or partially written) by two different XCDs.
+  int blk = blockIdx.x;
+  if ((gridDim.x & 7) == 0) blk = (blk & 7) * (gridDim.x >> 3) + (blk >> 3);
+  const int tile = blk % A.tiles;  // A.tiles = ceil(M / 16) here
+  const int n = blk / A.tiles;
+  const int N = A.N, V = A.V, M = A.M;
+  const long long VM = (long long)V * M;
+  const int m = tile * kRankTileM + q * 4;
+  const int rr = min(row, V - 1);
+  const bool live = row < V;
+  const unsigned lmask = live ? 0xffffffffu : 0u;
+  const yuma_params_t& pg = A.prm[n];
+  const bool liquid = pg.liquid_mode != YUMA_LIQUID_OFF;
+  const int reset_mode = pg.reset_mode, reset_epoch = pg.reset_epoch, reset_index = pg.reset_index;
+  const float p_bond_alpha = pg.bond_alpha, p_omba = pg.one_minus_bond_alpha;
+  const float p_maxint = pg.maxint, p_capacity_alpha = pg.capacity_alpha, p_decay_keep = pg.decay_keep;
+  // the reset test reads the previous epoch's consensus of one miner; it is
+  // known before the scan (phase 1 is done), so read it once here
+  bool reset_fire = false;
+  if (reset_mode != YUMA_RESET_NONE && reset_epoch >= A.t0 && reset_epoch < A.t1 &&
+      reset_index >= 0 && reset_index < M) {
+    reset_fire = reset_mode == YUMA_RESET_ALWAYS;
+    if (reset_mode == YUMA_RESET_IF_ZERO_CONSENSUS && reset_epoch >= 1)
+      reset_fire = A.C[((long long)(reset_epoch - 1) * N + n) * M + reset_index] == 0.0f;
+  }
+  const int reset_c = reset_index - m;  // column of this thread hit by a reset
+
+  float B[4];
+  bool has_old;
+  {
+    const float* src = A.t0 == 0 ? A.B_init : A.Bstate;
+    has_old = src != nullptr;
+    if (has_old)
+      load4c<VEC>(src + n * VM, rr, V, m, M, B);
+    else
+#pragma unroll
+      for (int c = 0; c < 4; ++c) B[c] = 0.0f;
+  }
+  // retire the bond-state load before the ring is filled (an s_waitcnt the
+  // compiler's waitcnt pass knows about: vmcnt(0)); otherwise its pending
+  // score survives the loop back-edge and every epoch would wait vmcnt(0)
+  __builtin_amdgcn_s_waitcnt(0x0F70);
+
+  float rw[P][4], rd[P], rsn[P], rc[P][4], rba[P][4];
+  auto fetch = [&](int k, int t) {
+    const long long slice = (long long)t * N + n;
+    load4c<VEC>(A.W + slice * VM, rr, V, m, M, rw[k]);
+    rd[k] = A.rsd[slice * V + rr];
+    rsn[k] = A.sn[slice * V + rr];
+    load4c<VEC>(A.C + slice * M, 0, 1, m, M, rc[k]);
+    if (liquid) load4c<VEC>(A.ba + slice * M, 0, 1, m, M, rba[k]);
+  };
+  // Every ring load is unconditional (epochs past the end re-read the last
+  // one): a load on only some paths into the loop header makes the waitcnt
+  // pass assume the shortest history and wait vmcnt(0) every epoch.
+#pragma unroll
+  for (int k = 0; k < P; ++k) fetch(k, min(A.t0 + k, A.t1 - 1));
+
+  float Bk[G][4];  // bond state after each epoch of the group
+  // epoch t = (group base) + k, its inputs in ring slot k % P
+  auto step = [&](int k, int t) {
+    const int sl = k % P;
+    const long long slice = (long long)t * N + n;
+    if (has_old && reset_fire && t == reset_epoch)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) B[c] = (c == reset_c) ? 0.0f : B[c];
+    float wn[4];
+    {
+      const RowDiv rdv = row_div(rd[sl]);
+      bool slow = false;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) wn[c] = div_fast(rw[sl][c], rdv, slow);
+      if (__any(slow)) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) wn[c] = rw[sl][c] / rd[sl];
+      }
+    }
+    // rank partials S * min(W, C) (yumas.py:439-442); rows >= V add 0 (a bit
+    // mask, not a branch)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const float x = rsn[sl] * vmin(wn[c], rc[sl][c]);
+      part[k][q * 4 + c][row] = __uint_as_float(__float_as_uint(x) & lmask);
+    }
+    if (VARIANT == YUMA_VARIANT_YUMA3) {
+      const float cap = rsn[sl] * p_maxint;
+      const float ca = p_capacity_alpha * cap;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const float rem = vmax(cap - B[c], 0.0f);
+        const float pc = vmin(ca, rem);
+        const float nb = p_decay_keep * B[c] + pc * wn[c];
+        B[c] = vmin(nb, cap);
+      }
+    } else {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const float bac = liquid ? rba[sl][c] : p_bond_alpha;
+        const float omba = liquid ? 1.0f - rba[sl][c] : p_omba;
+        const float bd = B[c] * omba;
+        const float rem = vmax(1.0f - bd, 0.0f);
+        const float nb = bd + vmin(bac * wn[c], rem);
+        B[c] = vmin(nb, 1.0f);
+      }
+    }
+    if (A.B_hist != nullptr && live)
+      store4<VEC>(A.B_hist + slice * VM + (long long)row * M, m, M, B);
+    has_old = true;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) Bk[k][c] = B[c];
+  };
+  // after the kn epochs of a group from tb: R, dividend partials, strip sums
+  auto finish = [&](int kn, int tb) {
+    __syncthreads();  // LDS only: the compiler emits lgkmcnt(0) + s_barrier
+    // wave w reduces (epoch, miner) pairs w, w + nw, ...
+    for (int j = wave; j < kn * kRankTileM; j += nw) {
+      const int k = j / kRankTileM, mm = j % kRankTileM;
+      float a = 0.0f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (lane + 64 * i < V) a = a + part[k][mm][lane + 64 * i];
+      a = wave_sum(a);
+      if (lane == 0) {
+        rsh[k][mm] = a;
+        const int mg = tile * kRankTileM + mm;
+        if (mg < M) A.R[((long long)(tb + k) * N + n) * M + mg] = a;
+      }
+    }
+    __syncthreads();
+    // dividend partials sum_m B R over the strip
+#pragma unroll
+    for (int k = 0; k < G; ++k) {
+      if (k < kn) {
+        const long long sp = (long long)(tb + k) * N + n;
+        const float4 r4 = *reinterpret_cast<const float4*>(&rsh[k][q * 4]);
+        const float rv[4] = {r4.x, r4.y, r4.z, r4.w};
+        float d = 0.0f;
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          if (m + c < M) d = d + Bk[k][c] * rv[c];
+        d = d + __shfl_xor(d, 1, 64);
+        d = d + __shfl_xor(d, 2, 64);
+        if (q == 0 && live) A.dpart[(sp * A.tiles + tile) * V + row] = d;
+      }
+    }
+    // the strip's rank sums (16 miners, fixed butterfly)
+    if (wave == 0) {
+#pragma unroll
+      for (int k0 = 0; k0 < G; k0 += 4) {
+        const int k = k0 + (lane >> 4), mm = lane & 15;
+        float s = (k < kn && tile * kRankTileM + mm < M) ? rsh[k][mm] : 0.0f;
+        s = s + __shfl_xor(s, 1, 64);
+        s = s + __shfl_xor(s, 2, 64);
+        s = s + __shfl_xor(s, 4, 64);
+        s = s + __shfl_xor(s, 8, 64);
+        if (mm == 0 && k < kn) A.rpart[((long long)(tb + k) * N + n) * A.tiles + tile] = s;
+      }
+    }
+  };
+
+  int tb = A.t0;
+  for (; tb + G <= A.t1; tb += G) {
+#pragma unroll
+    for (int k = 0; k < G; ++k) {
+      step(k, tb + k);
+      fetch(k % P, min(tb + k + P, A.t1 - 1));
+    }
+    finish(G, tb);
+  }
+  if (tb < A.t1) {  // the last partial group
+    const int kn = A.t1 - tb;
+#pragma unroll
+    for (int k = 0; k < G; ++k)
+      if (k < kn) {
+        step(k, tb + k);
+        fetch(k % P, min(tb + k + P, A.t1 - 1));
+      }
+    finish(kn, tb);
+  }
+  if (live) store4<VEC>(A.Bstate + n * VM + (long long)row * M, m, M, B);
 }
 
 // ---------------------------------------------------------------------------
@@ -2058,7 +2299,8 @@ __global__ __launch_bounds__(256) void k_finalize(const float* __restrict__ dpar
                                                   const float* __restrict__ tvc,
                                                   const float* __restrict__ tvn,
                                                   float* __restrict__ Dn, float* __restrict__ D,
-                                                  float* __restrict__ Tv) {
+                                                  float* __restrict__ Tv,
+                                                  const float* __restrict__ rdiv_scal = nullptr) {
   // thread (tg, vq): tile group tg = tid / 64 sums tiles tg, tg+4, ...; vq owns
   // validators 4vq..4vq+3 of the current 256-validator window. Fixed order:
   // per-group sequential, then groups 0..3.
@@ -2087,6 +2329,12 @@ __global__ __launch_bounds__(256) void k_finalize(const float* __restrict__ dpar
         d = d + part[1][j];
         d = d + part[2][j];
         d = d + part[3][j];
+        if (rdiv_scal != nullptr) {
+          // k_bonds_rank partials are sum_m B R: divide by R.sum() once. I =
+          // nan_to_num(R / R.sum()) is all zero when R.sum() is 0 or not finite
+          const float sr = rdiv_scal[slice * 8 + 5];
+          d = (sr == 0.0f || !isfinite(sr)) ? 0.0f : d / sr;
+        }
         if (variant == YUMA_VARIANT_YUMA4) d = sn[slice * V + v] * d;
         dsh[v] = d;
       }
@@ -2246,8 +2494,13 @@ struct Workspace {
   size_t bytes;
 };
 
+// YUMA_RANKFUSE=1: fold the rank pass into the Yuma3/4 bond scan (k_bonds_rank)
+bool rankfuse_knob() {
+  const char* rf = getenv("YUMA_RANKFUSE");
+  return rf != nullptr && rf[0] == '1';
+}
+
 Workspace carve(char* base, int variant, int N, int E, int V, int M, int full) {
-  (void)variant;
   Workspace w{};
   const size_t S = (size_t)E * N;
   const size_t tiles = (size_t)(M + yk::kTileM - 1) / yk::kTileM;
@@ -2265,8 +2518,12 @@ Workspace carve(char* base, int variant, int N, int E, int V, int M, int full) {
   w.R = (float*)take(S * M * 4);
   w.I = (float*)take(S * M * 4);
   w.ba = (float*)take(S * M * 4);
-  w.rpart = (float*)take(S * tiles * 4);
-  w.dpart = (float*)take(S * tiles * V * 4);
+  // k_bonds_rank (Yuma3/4, run outputs) keeps per-16-miner-strip partials
+  const size_t ptiles = (rankfuse_knob() && variant >= YUMA_VARIANT_YUMA3 && !full && V <= 256)
+                            ? (size_t)(M + yk::kRankTileM - 1) / yk::kRankTileM
+                            : tiles;
+  w.rpart = (float*)take(S * ptiles * 4);
+  w.dpart = (float*)take(S * ptiles * V * 4);
   w.scal = (float*)take(S * 8 * 4);
   w.tvc = full ? (float*)take(S * tiles * V * 4) : nullptr;
   w.tvn = full ? (float*)take(S * tiles * V * 4) : nullptr;
@@ -2455,10 +2712,15 @@ int bonds_knob() {
     const char* e = getenv("YUMA_BONDS");
     knob = 0;
     if (e != nullptr) {
-      if (!strcmp(e, "p8")) knob = 1;
+      if (!strcmp(e, "p4")) knob = 9;
+      else if (!strcmp(e, "p8")) knob = 1;
       else if (!strcmp(e, "p4nt")) knob = 2;
       else if (!strcmp(e, "p8nt")) knob = 3;
       else if (!strcmp(e, "p4v")) knob = 4;
+      else if (!strcmp(e, "p2")) knob = 5;
+      else if (!strcmp(e, "p4w4")) knob = 6;
+      else if (!strcmp(e, "p4w5")) knob = 7;
+      else if (!strcmp(e, "p2w5")) knob = 8;
     }
   }
   return knob;
@@ -2471,7 +2733,11 @@ void launch_bonds_elem(int R, long long nblocks, hipStream_t st, const yk::BondA
     case 2: YK_LAUNCH((yk::k_bonds_elem<VARIANT, 1, VEC, 4, true>), nblocks, 256, st, A); break;
     case 3: YK_LAUNCH((yk::k_bonds_elem<VARIANT, 1, VEC, 8, true>), nblocks, 256, st, A); break;
     case 4: YK_LAUNCH((yk::k_bonds_elem<VARIANT, 1, VEC, 4, false, VEC>), nblocks, 256, st, A); break;
-    default: YK_LAUNCH((yk::k_bonds_elem<VARIANT, 1, VEC, 4, false>), nblocks, 256, st, A); break;
+    case 9: YK_LAUNCH((yk::k_bonds_elem<VARIANT, 1, VEC, 4, false>), nblocks, 256, st, A); break;
+    case 6: YK_LAUNCH((yk::k_bonds_elem<VARIANT, 1, VEC, 4, false, false, 4>), nblocks, 256, st, A); break;
+    case 7: YK_LAUNCH((yk::k_bonds_elem<VARIANT, 1, VEC, 4, false, false, 5>), nblocks, 256, st, A); break;
+    case 8: YK_LAUNCH((yk::k_bonds_elem<VARIANT, 1, VEC, 2, false, false, 5>), nblocks, 256, st, A); break;
+    default: YK_LAUNCH((yk::k_bonds_elem<VARIANT, 1, VEC, 2, false>), nblocks, 256, st, A); break;
   }
 }
 
@@ -2495,6 +2761,21 @@ void launch_bonds(int variant, RowCfg rc, int elemR, long long nblocks, hipStrea
       launch_bonds_elem<YUMA_VARIANT_YUMA4, VEC>(elemR, nblocks, st, A);
       break;
   }
+}
+
+void launch_bonds_rank(int variant, bool vec, long long nblocks, int threads, hipStream_t st,
+                       const yk::BondArgs& A) {
+  // YUMA_RANKG=4: 4 instead of 8 epochs per barrier pair for Yuma3 (A/B knob)
+  const char* g = getenv("YUMA_RANKG");
+  const bool g4 = g != nullptr && g[0] == '4';
+#define YK_BR(VAR, VEC_, G_) YK_LAUNCH((yk::k_bonds_rank<VAR, VEC_, yk::kRankP, G_>), nblocks, threads, st, A)
+  if (variant == YUMA_VARIANT_YUMA3) {
+    if (g4) { if (vec) YK_BR(YUMA_VARIANT_YUMA3, true, 4); else YK_BR(YUMA_VARIANT_YUMA3, false, 4); }
+    else { if (vec) YK_BR(YUMA_VARIANT_YUMA3, true, 8); else YK_BR(YUMA_VARIANT_YUMA3, false, 8); }
+  } else {  // Yuma4's liquid-alpha ring slots leave no room for 8 bond states
+    if (vec) YK_BR(YUMA_VARIANT_YUMA4, true, 4); else YK_BR(YUMA_VARIANT_YUMA4, false, 4);
+  }
+#undef YK_BR
 }
 
 // Optional per-phase timing (bench / roofline): a HIP event is recorded on the
@@ -2635,6 +2916,17 @@ int run_impl(int variant, const yuma_params_t* prm, int N, int E, int V, int M, 
   const bool fused = variant != YUMA_VARIANT_YUMA2 && tiles * 2 <= device_cus() &&
                      fz != nullptr && fz[0] == '1';
 
+  // rank folded into the bond scan (k_bonds_rank): Yuma3/4 run outputs with
+  // V <= 256 (one block per 16-miner strip holds every row). Small subnets
+  // (M < 64, e.g. the dividend sheet's 3 x 2 cases) keep the separate rank
+  // pass so their reported dividends round exactly as the reference's.
+  // Opt-in (YUMA_RANKFUSE=1): measured slower than the separate rank pass on
+  // MI355X at c2 (rank+bonds 2.72-2.80 ms vs 0.97 + 1.81): a
+  // full-column block forces 16-miner strips, i.e. 64-B row segments.
+  const bool rankfuse = variant >= YUMA_VARIANT_YUMA3 && !full && V <= 256 && M >= 64 &&
+                        out->Wn == nullptr && out->Wc == nullptr && !fused && rankfuse_knob();
+  const int stiles = (M + yk::kRankTileM - 1) / yk::kRankTileM;
+
   PhaseTimer tm{};
   tm.ms = phase_ms;
   tm.st = st;
@@ -2712,6 +3004,7 @@ int run_impl(int variant, const yuma_params_t* prm, int N, int E, int V, int M, 
     YK_LAUNCH(yk::k_quantise<256>, ns, 256, st, ws.craw, prm, variant, N, M, s0, C, ws.qlev,
               ba_buf, ws.scal, nullptr, nullptr, 0);
     if (sb != st && !stream_edge(st, sb)) return fail(YUMA_EHIP, "stream edge failed");
+    if (!rankfuse) {
     tm.mark(3);
     if (vec)
       launch_rank<true>(rc, ns * tiles, sb, W, ws.rsd, ws.sn, C, Wprev_init,
@@ -2724,6 +3017,7 @@ int run_impl(int variant, const yuma_params_t* prm, int N, int E, int V, int M, 
     tm.mark(4);
     YK_LAUNCH(yk::k_incentive, ns, 256, sb, out->R ? out->R : ws.R, ws.rpart, out->P, M, s0,
               tiles, I, out->P ? out->T : nullptr, ws.scal, nullptr);
+    }
     }
 
     yk::BondArgs A{};
@@ -2750,6 +3044,19 @@ int run_impl(int variant, const yuma_params_t* prm, int N, int E, int V, int M, 
     A.t1 = c1;
     const long long nb = (long long)N * tiles * rowblocks;
     tm.mark(5);
+    if (rankfuse) {
+      A.tiles = stiles;
+      A.rowblocks = 1;
+      A.R = out->R ? out->R : ws.R;
+      A.rpart = ws.rpart;
+      launch_bonds_rank(variant, vec, (long long)N * stiles, (V + 15) / 16 * 64, sb, A);
+      tm.mark(4);
+      YK_LAUNCH(yk::k_incentive, ns, 256, sb, A.R, ws.rpart, out->P, M, s0, stiles, I,
+                out->P ? out->T : nullptr, ws.scal, nullptr);
+      tm.mark(6);
+      YK_LAUNCH(yk::k_finalize, ns, 256, sb, ws.dpart, ws.sn, variant, V, s0, stiles, ws.tvc,
+                ws.tvn, out->Dn, out->D, out->Tv, ws.scal);
+    } else {
     if (vec)
       launch_bonds<true>(variant, rc, elemR, nb, sb, A);
     else
@@ -2757,6 +3064,7 @@ int run_impl(int variant, const yuma_params_t* prm, int N, int E, int V, int M, 
     tm.mark(6);
     YK_LAUNCH(yk::k_finalize, ns, 256, sb, ws.dpart, ws.sn, variant, V, s0, tiles, ws.tvc,
               ws.tvn, out->Dn, out->D, out->Tv);
+    }
     if (out->Sn != nullptr)
       (void)hipMemcpyAsync(out->Sn + s0 * V, ws.sn + s0 * V, (size_t)ns * V * 4,
                            hipMemcpyDeviceToDevice, sb);
