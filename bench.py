@@ -199,8 +199,15 @@ def bench_engine(args, world: int, rank: int, dist: bool) -> dict:
     ws = torch.empty(engine.workspace_bytes(variant, N, E, V, M, False), dtype=torch.uint8, device=dev)
     chunk = args.chunk
 
-    def step():
-        return engine.run(variant, params, W, S, want_hist=hist, out=out, workspace=ws, chunk_epochs=chunk)
+    if args.no_graph:
+        def step():
+            return engine.run(variant, params, W, S, want_hist=hist, out=out, workspace=ws, chunk_epochs=chunk)
+    else:
+        # the whole E-epoch run captured once into a HIP graph (yuma_graph_create);
+        # each timed step is one replay of it over the same resident inputs
+        graph = engine.RunGraph(variant, params, W, S, want_hist=hist, out=out, workspace=ws,
+                                chunk_epochs=chunk)
+        step = graph.launch
 
     elapsed = timed(step, args.warmup, args.steps, dist, dev)
     value = float(E) * N * world * args.steps / elapsed
@@ -231,7 +238,7 @@ def bench_engine(args, world: int, rank: int, dist: bool) -> dict:
     else:
         wl = f"c2: single subnet {V}V x {M}M x {E} epochs, {args.version}" + (" liquid" if liquid else "")
     workload = {"workload": wl, "V": V, "M": M, "epochs": E, "scenarios_per_gpu": N, "version": args.version,
-                "bond_history": hist,
+                "bond_history": hist, "launch": "direct" if args.no_graph else "hipGraph replay",
                 "parallelism": f"scenario-sharded x{world}" if world > 1 else "single GPU"}
     traffic = load_traffic({k: workload[k] for k in ("V", "M", "epochs", "version", "bond_history")}, dom_name)
     line = base_line(args, world, value, "scenario-epochs/s", elapsed, "weak", workload)
@@ -384,6 +391,8 @@ def main():
     ap.add_argument("--liquid", action="store_true")
     ap.add_argument("--no-history", action="store_true", help="do not write every epoch's bond state")
     ap.add_argument("--chunk", type=int, default=0, help="epochs per phase-1 batch (0 = engine default)")
+    ap.add_argument("--no-graph", action="store_true",
+                    help="c2/c3: launch each step directly instead of replaying a captured hipGraph")
     ap.add_argument("--seed", type=lambda s: int(s, 0), default=None)
     ap.add_argument("--cpu-epochs", type=int, default=400)
     ap.add_argument("--no-cpu-baseline", action="store_true")

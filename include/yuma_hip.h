@@ -144,6 +144,26 @@ int yuma_run(int variant, const yuma_params_t* params_dev, int N, int E, int V, 
              const yuma_outputs_t* out, void* workspace, size_t workspace_bytes,
              int chunk_epochs, void* stream);
 
+/* hipGraph form of yuma_run: the whole multi-epoch run (every phase of every
+ * chunk, no host work between them) captured once into a HIP graph and
+ * replayed with one hipGraphLaunch. The arguments are those of yuma_run and
+ * are baked into the graph: every replay reads the same W / S / params /
+ * B_init buffers (refill them in place between replays) and writes the same
+ * outputs. Capture happens on an internal stream; `stream` orders the capture
+ * after the caller's prior work only through the caller's own sync, so call
+ * it with inputs already resident. Replaces the per-epoch Python loop of
+ * run_simulation (simulation_utils.py:52-110) for repeated runs.            */
+typedef struct yuma_graph* yuma_graph_t;
+int yuma_graph_create(yuma_graph_t* graph, int variant, const yuma_params_t* params_dev, int N,
+                      int E, int V, int M, const float* W, const float* S,
+                      const float* B_init, const float* Wprev_init, const yuma_outputs_t* out,
+                      void* workspace, size_t workspace_bytes, int chunk_epochs);
+/* Replay on `stream` (stream-ordered, no host synchronisation). */
+int yuma_graph_launch(yuma_graph_t graph, void* stream);
+/* Kernel nodes in the captured graph (diagnostics / tests). */
+int yuma_graph_nodes(yuma_graph_t graph);
+int yuma_graph_destroy(yuma_graph_t graph);
+
 /* Phases of a run, in launch order (per chunk of epochs). */
 enum yuma_phase {
   YUMA_PHASE_ROWSUM = 0,    /* k_rowsum:    row sums, stake normalisation      */

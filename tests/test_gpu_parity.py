@@ -418,3 +418,29 @@ def test_rank_folded_into_bond_scan_matches_separate_pass(V, M, monkeypatch):
         np.testing.assert_array_equal(a.C[:, 0].cpu().numpy(), ref["C"])
         assert_close(a.Dn[:, 0].cpu().numpy(), ref["Dn"], what=f"{tag} Dn vs oracle")
         assert_close(a.I[:, 0].cpu().numpy(), ref["I"], what=f"{tag} I vs oracle")
+
+
+@pytest.mark.parametrize("variant,chunk", [("yuma3", 0), ("yuma4", 5), ("yuma1", 0), ("yuma2", 4)])
+def test_graph_replay_equals_direct_run(variant, chunk):
+    """yuma_graph_create captures a whole multi-epoch run into one HIP graph;
+    every replay must equal a direct yuma_run bitwise, including after the
+    inputs are refilled in place, and the graph holds only device work
+    (no host nodes): one kernel per phase per chunk."""
+    E, N, V, M = 12, 2, 64, 512
+    W = torch.from_numpy(synth.weights(0x6A, E, N, V, M)).cuda()
+    S = torch.from_numpy(synth.stakes(0x6A, E, N, V, period=3)).cuda()
+    vid = VARIANT_ID[variant]
+    cfg = config_from({"liquid_alpha": True} if variant == "yuma4" else {})
+    prm = [engine.make_params(vid, cfg)] * N
+    g = engine.RunGraph(vid, prm, W, S, want_hist=True, chunk_epochs=chunk)
+    assert g.nodes() >= 7
+    for seed in (0x6A, 0x6B):
+        W.copy_(torch.from_numpy(synth.weights(seed, E, N, V, M)))
+        S.copy_(torch.from_numpy(synth.stakes(seed, E, N, V, period=3)))
+        r = g.launch()
+        ref = engine.run(vid, prm, W, S, want_hist=True, chunk_epochs=chunk)
+        torch.cuda.synchronize()
+        for a, b in ((r.Dn, ref.Dn), (r.C, ref.C), (r.I, ref.I), (r.B_hist, ref.B_hist),
+                     (r.B_final, ref.B_final)):
+            assert torch.equal(a, b)
+    g.close()

@@ -67,6 +67,11 @@ __device__ __forceinline__ float tmax(float a, float b) {
   if (a != a || b != b) return qnan();
   return b > a ? b : a;
 }
+// torch.minimum / torch.maximum in one instruction (gfx950 v_minimum3_f32 /
+// v_maximum3_f32, NaN-propagating); unlike tmin/tmax they order -0 < +0,
+// which no sum, product or comparison downstream can tell apart
+__device__ __forceinline__ float vmin(float a, float b) { return __builtin_elementwise_minimum(a, b); }
+__device__ __forceinline__ float vmax(float a, float b) { return __builtin_elementwise_maximum(a, b); }
 // torch.nan_to_num(x, nan=nan_v): +-inf -> +-FLT_MAX.
 __device__ __forceinline__ float nan_to_num(float x, float nan_v = 0.0f) {
   if (x != x) return nan_v;
@@ -644,10 +649,10 @@ __global__ __launch_bounds__(256) void k_consensus_w(const float* __restrict__ W
       stot = stot + s[i];
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
-        const float x = wn[i][c];
-        vmax[c] = x > vmax[c] ? x : vmax[c];
-        const float xm = x == x ? x : 0.0f;
-        vmin[c] = xm < vmin[c] ? xm : vmin[c];
+        // NaN-ignoring max (v_max3 pairs); NaN and negatives count as 0 for
+        // the min: gmin below only asks whether it is > 0
+        vmax[c] = fmaxf(vmax[c], wn[i][c]);
+        vmin[c] = fminf(vmin[c], fmaxf(wn[i][c], 0.0f));
       }
     }
     // F(k) with every mask set, in exactly the order every F below uses
@@ -759,7 +764,7 @@ __global__ __launch_bounds__(256) void k_rank_w(
     source(i, src);
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-      wc[c] = tmin(src[c], Cc[c]);
+      wc[c] = vmin(src[c], Cc[c]);
       acc[c] = acc[c] + s[i] * wc[c];
     }
     if (FULL && row < V) {
@@ -792,7 +797,7 @@ __global__ __launch_bounds__(256) void k_rank_w(
 #pragma unroll
       for (int c = 0; c < 4; ++c)
         if (m + c < M) {
-          a = a + tmin(src[c], Cc[c]);
+          a = a + vmin(src[c], Cc[c]);
           b = b + wn[i][c];
         }
       a = qsum4(a);
@@ -1906,10 +1911,8 @@ __global__ __launch_bounds__(NT) void k_bonds(BondArgs A) {
 // (a register ring refilled as each epoch is consumed), so the per-epoch HBM
 // latency is hidden behind P-1 epochs of work.
 // ---------------------------------------------------------------------------
-// WPE: minimum waves per SIMD the register allocation must allow (0 = free)
-template <int VARIANT, int R, bool VEC, int P, bool NTS, bool VECI = false, int WPE = 0>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? WPE : 1)))
-void k_bonds_elem(BondArgs A) {
+template <int VARIANT, int R, bool VEC, int P, bool NTS, bool VECI = false>
+__global__ __launch_bounds__(256) void k_bonds_elem(BondArgs A) {
   constexpr int G = 16;
   const Lay L = lay();
   const int tile = blockIdx.x % A.tiles;
@@ -1934,25 +1937,14 @@ void k_bonds_elem(BondArgs A) {
     has_old = src != nullptr;
 #pragma unroll
     for (int i = 0; i < R; ++i) {
-      if (has_old)
-        load4c<VEC>(src + n * VM, row0 + G * i, V, m, M, B[i]);
+      const int row = row0 + G * i;
+      if (has_old && row < V)
+        load4<VEC>(src + n * VM + (long long)row * M, m, M, B[i]);
       else
 #pragma unroll
         for (int c = 0; c < 4; ++c) B[i][c] = 0.0f;
     }
   }
-  // The reset test (the previous epoch's consensus of one miner) is known
-  // before the scan: read it here, not inside the ring loop.
-  bool reset_fire = false;
-  if (reset_mode != YUMA_RESET_NONE && reset_epoch >= A.t0 && reset_epoch < A.t1 &&
-      reset_index >= 0 && reset_index < M) {
-    reset_fire = reset_mode == YUMA_RESET_ALWAYS;
-    if (reset_mode == YUMA_RESET_IF_ZERO_CONSENSUS && reset_epoch >= 1)
-      reset_fire = A.C[((long long)(reset_epoch - 1) * N + n) * M + reset_index] == 0.0f;
-  }
-  // retire these loads before the ring fills (vmcnt(0), an s_waitcnt the
-  // compiler's waitcnt pass sees), or their scores survive the loop back-edge
-  __builtin_amdgcn_s_waitcnt(0x0F70);
 
   float rw[P][R][4], rd[P][R], rsn[P][R], ri[P][4], rba[P][4];
   auto fetch = [&](int k, int t) {
@@ -1973,21 +1965,28 @@ void k_bonds_elem(BondArgs A) {
       if (liquid) vec4raw(A.ba + slice * M, m, M, rba[k]);
     }
   };
-  // Every ring load is unconditional (epochs past the end re-read the last
-  // one) and the main loop runs whole ring turns only: a load on some paths
-  // into the loop header makes the waitcnt pass assume the shortest history
-  // and wait vmcnt(0) every epoch, i.e. drain the ring.
 #pragma unroll
-  for (int k = 0; k < P; ++k) fetch(k, min(A.t0 + k, A.t1 - 1));
+  for (int k = 0; k < P; ++k)
+    if (A.t0 + k < A.t1) fetch(k, A.t0 + k);
 
-  auto step = [&](int k, int t) {
+  for (int tb = A.t0; tb < A.t1; tb += P) {
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+      const int t = tb + k;
+      if (t >= A.t1) break;
       const long long slice = (long long)t * N + n;
-      if (has_old && reset_fire && t == reset_epoch) {
+      if (has_old && reset_mode != YUMA_RESET_NONE && t == reset_epoch && reset_index >= 0 &&
+          reset_index < M) {
+        bool fire = reset_mode == YUMA_RESET_ALWAYS;
+        if (reset_mode == YUMA_RESET_IF_ZERO_CONSENSUS && t >= 1)
+          fire = A.C[(slice - N) * M + reset_index] == 0.0f;
         const int c = reset_index - m;
+        if (fire && c >= 0 && c < 4)
 #pragma unroll
-        for (int i = 0; i < R; ++i)
+          for (int i = 0; i < R; ++i)
 #pragma unroll
-          for (int cc = 0; cc < 4; ++cc) B[i][cc] = (cc == c) ? 0.0f : B[i][cc];
+            for (int cc = 0; cc < 4; ++cc)
+              if (cc == c) B[i][cc] = 0.0f;
       }
       float bac[4], omba[4];
 #pragma unroll
@@ -2045,18 +2044,9 @@ void k_bonds_elem(BondArgs A) {
         if (L.c4 == 0 && row < V) A.dpart[(slice * A.tiles + tile) * V + row] = d;
       }
       has_old = true;
-  };
-  int tb = A.t0;
-  for (; tb + P <= A.t1; tb += P) {
-#pragma unroll
-    for (int k = 0; k < P; ++k) {
-      step(k, tb + k);
-      fetch(k, min(tb + k + P, A.t1 - 1));
+      if (t + P < A.t1) fetch(k, t + P);
     }
   }
-#pragma unroll
-  for (int k = 0; k < P; ++k)  // the last partial turn: inputs already in the ring
-    if (tb + k < A.t1) step(k, tb + k);
 #pragma unroll
   for (int i = 0; i < R; ++i) {
     const int row = row0 + G * i;
@@ -2083,12 +2073,6 @@ void k_bonds_elem(BondArgs A) {
 // in registers. Two barriers per P epochs keep the waves loosely coupled; the
 // prefetch ring stays in flight across them (no vmcnt drain at a barrier).
 // ---------------------------------------------------------------------------
-// torch.minimum / torch.maximum in one instruction (gfx950 v_minimum3_f32 /
-// v_maximum3_f32, NaN-propagating); unlike tmin/tmax they order -0 < +0,
-// which no sum, product or comparison downstream can tell apart
-__device__ __forceinline__ float vmin(float a, float b) { return __builtin_elementwise_minimum(a, b); }
-__device__ __forceinline__ float vmax(float a, float b) { return __builtin_elementwise_maximum(a, b); }
-
 constexpr int kRankTileM = 16;  // miners per column strip
 constexpr int kRankLdsV = 260;  // padded row stride of the partial tile (banks)
 constexpr int kRankP = 4;       // prefetch depth (epochs in flight)
@@ -2712,15 +2696,10 @@ int bonds_knob() {
     const char* e = getenv("YUMA_BONDS");
     knob = 0;
     if (e != nullptr) {
-      if (!strcmp(e, "p4")) knob = 9;
-      else if (!strcmp(e, "p8")) knob = 1;
+      if (!strcmp(e, "p8")) knob = 1;
       else if (!strcmp(e, "p4nt")) knob = 2;
       else if (!strcmp(e, "p8nt")) knob = 3;
       else if (!strcmp(e, "p4v")) knob = 4;
-      else if (!strcmp(e, "p2")) knob = 5;
-      else if (!strcmp(e, "p4w4")) knob = 6;
-      else if (!strcmp(e, "p4w5")) knob = 7;
-      else if (!strcmp(e, "p2w5")) knob = 8;
     }
   }
   return knob;
@@ -2733,11 +2712,7 @@ void launch_bonds_elem(int R, long long nblocks, hipStream_t st, const yk::BondA
     case 2: YK_LAUNCH((yk::k_bonds_elem<VARIANT, 1, VEC, 4, true>), nblocks, 256, st, A); break;
     case 3: YK_LAUNCH((yk::k_bonds_elem<VARIANT, 1, VEC, 8, true>), nblocks, 256, st, A); break;
     case 4: YK_LAUNCH((yk::k_bonds_elem<VARIANT, 1, VEC, 4, false, VEC>), nblocks, 256, st, A); break;
-    case 9: YK_LAUNCH((yk::k_bonds_elem<VARIANT, 1, VEC, 4, false>), nblocks, 256, st, A); break;
-    case 6: YK_LAUNCH((yk::k_bonds_elem<VARIANT, 1, VEC, 4, false, false, 4>), nblocks, 256, st, A); break;
-    case 7: YK_LAUNCH((yk::k_bonds_elem<VARIANT, 1, VEC, 4, false, false, 5>), nblocks, 256, st, A); break;
-    case 8: YK_LAUNCH((yk::k_bonds_elem<VARIANT, 1, VEC, 2, false, false, 5>), nblocks, 256, st, A); break;
-    default: YK_LAUNCH((yk::k_bonds_elem<VARIANT, 1, VEC, 2, false>), nblocks, 256, st, A); break;
+    default: YK_LAUNCH((yk::k_bonds_elem<VARIANT, 1, VEC, 4, false>), nblocks, 256, st, A); break;
   }
 }
 
@@ -3235,6 +3210,11 @@ int shard_stage_impl(int stage, int variant, const yuma_params_t* prm, int N, in
 
 }  // namespace
 
+struct yuma_graph {
+  hipGraph_t graph;
+  hipGraphExec_t exec;
+};
+
 extern "C" {
 
 size_t yuma_workspace_bytes(int variant, int N, int E, int V, int M, int full_outputs) {
@@ -3287,6 +3267,62 @@ int yuma_shard_stage(int stage, int variant, const yuma_params_t* params_dev, in
                      void* stream) {
   return shard_stage_impl(stage, variant, params_dev, N, E, V, M, W, S, B_init, Wprev_init, io,
                           out, workspace, workspace_bytes, stream);
+}
+
+int yuma_graph_create(yuma_graph_t* graph, int variant, const yuma_params_t* params_dev, int N,
+                      int E, int V, int M, const float* W, const float* S,
+                      const float* B_init, const float* Wprev_init, const yuma_outputs_t* out,
+                      void* workspace, size_t workspace_bytes, int chunk_epochs) {
+  if (graph == nullptr) return fail(YUMA_EINVAL, "graph handle pointer is NULL");
+  *graph = nullptr;
+  hipStream_t cs = nullptr;
+  if (hipStreamCreateWithFlags(&cs, hipStreamNonBlocking) != hipSuccess)
+    return fail(YUMA_EHIP, "capture stream creation failed");
+  if (hipStreamBeginCapture(cs, hipStreamCaptureModeRelaxed) != hipSuccess) {
+    (void)hipStreamDestroy(cs);
+    return fail(YUMA_EHIP, "hipStreamBeginCapture failed");
+  }
+  const int rc = run_impl(variant, params_dev, N, E, V, M, W, S, B_init, Wprev_init, out,
+                          workspace, workspace_bytes, chunk_epochs, cs);
+  hipGraph_t g = nullptr;
+  const hipError_t ec = hipStreamEndCapture(cs, &g);
+  (void)hipStreamDestroy(cs);
+  if (rc != YUMA_OK) {
+    if (g) (void)hipGraphDestroy(g);
+    return rc;  // run_impl's message stands
+  }
+  if (ec != hipSuccess || g == nullptr)
+    return fail(YUMA_EHIP, "hipStreamEndCapture failed: %s", hipGetErrorString(ec));
+  hipGraphExec_t x = nullptr;
+  if (hipGraphInstantiate(&x, g, nullptr, nullptr, 0) != hipSuccess) {
+    (void)hipGraphDestroy(g);
+    return fail(YUMA_EHIP, "hipGraphInstantiate failed");
+  }
+  *graph = new yuma_graph{g, x};
+  return YUMA_OK;
+}
+
+int yuma_graph_launch(yuma_graph_t graph, void* stream) {
+  if (graph == nullptr) return fail(YUMA_EINVAL, "NULL graph");
+  const hipError_t e = hipGraphLaunch(graph->exec, (hipStream_t)stream);
+  if (e != hipSuccess) return fail(YUMA_EHIP, "hipGraphLaunch failed: %s", hipGetErrorString(e));
+  return YUMA_OK;
+}
+
+int yuma_graph_nodes(yuma_graph_t graph) {
+  if (graph == nullptr) return fail(YUMA_EINVAL, "NULL graph");
+  size_t n = 0;
+  if (hipGraphGetNodes(graph->graph, nullptr, &n) != hipSuccess)
+    return fail(YUMA_EHIP, "hipGraphGetNodes failed");
+  return (int)n;
+}
+
+int yuma_graph_destroy(yuma_graph_t graph) {
+  if (graph == nullptr) return YUMA_OK;
+  (void)hipGraphExecDestroy(graph->exec);
+  (void)hipGraphDestroy(graph->graph);
+  delete graph;
+  return YUMA_OK;
 }
 
 const char* yuma_last_error(void) { return g_err; }

@@ -41,6 +41,10 @@ EXPORTED_SYMBOLS = (
     "yuma_epoch",
     "yuma_synth_weights",
     "yuma_shard_stage",
+    "yuma_graph_create",
+    "yuma_graph_launch",
+    "yuma_graph_nodes",
+    "yuma_graph_destroy",
     "yuma_last_error",
     "yuma_version",
 )
@@ -139,6 +143,16 @@ def load_library(path: str | None = None):
         lib.yuma_shard_stage.restype = i32
         lib.yuma_synth_weights.argtypes = [ctypes.c_uint64, i32, i32, i32, i32, i32, vp, vp]
         lib.yuma_synth_weights.restype = i32
+        if hasattr(lib, "yuma_graph_create"):  # absent only in older A/B builds (YUMA_LIB)
+            lib.yuma_graph_create.argtypes = [ctypes.POINTER(vp), i32, vp, i32, i32, i32, i32, vp, vp,
+                                              vp, vp, vp, vp, sz, i32]
+            lib.yuma_graph_create.restype = i32
+            lib.yuma_graph_launch.argtypes = [vp, vp]
+            lib.yuma_graph_launch.restype = i32
+            lib.yuma_graph_nodes.argtypes = [vp]
+            lib.yuma_graph_nodes.restype = i32
+            lib.yuma_graph_destroy.argtypes = [vp]
+            lib.yuma_graph_destroy.restype = i32
         lib.yuma_last_error.argtypes = []
         lib.yuma_last_error.restype = ctypes.c_char_p
         lib.yuma_version.argtypes = []
@@ -271,7 +285,7 @@ def run(variant: int, params: list[YumaParamsC], W: torch.Tensor, S: torch.Tenso
         B_init: torch.Tensor | None = None, Wprev_init: torch.Tensor | None = None, *,
         want_hist: bool = False, want: tuple[str, ...] = (), chunk_epochs: int = 0,
         workspace: torch.Tensor | None = None, out: dict | None = None,
-        phase_ms: list | None = None) -> RunResult:
+        phase_ms: list | None = None, capture: list | None = None) -> RunResult:
     """E epochs of N scenarios. W [E,N,V,M], S [E,N,V] (raw); optional
     B_init [N,V,M] and (Yuma2) normalised Wprev_init [N,V,M]."""
     dev = device()
@@ -316,7 +330,12 @@ def run(variant: int, params: list[YumaParamsC], W: torch.Tensor, S: torch.Tenso
     args = (variant, prm.data_ptr(), N, E, V, M, W.data_ptr(), S.data_ptr(),
             _ptr(B_init), _ptr(Wprev_init), ctypes.addressof(outs),
             workspace.data_ptr(), workspace.numel(), int(chunk_epochs), stream)
-    if phase_ms is None:
+    if capture is not None:  # RunGraph: capture instead of launching
+        h = ctypes.c_void_p()
+        torch.cuda.synchronize(dev)
+        _check(lib.yuma_graph_create(ctypes.byref(h), *args[:-1]), "yuma_graph_create")
+        capture.append(h)
+    elif phase_ms is None:
         _check(lib.yuma_run(*args), "yuma_run")
     else:  # bench-only: per-phase device time from HIP events (blocks)
         buf = (ctypes.c_float * len(PHASES))()
@@ -326,6 +345,40 @@ def run(variant: int, params: list[YumaParamsC], W: torch.Tensor, S: torch.Tenso
     # keep inputs alive until the stream has consumed them
     keep["_inputs"] = (W, S, B_init, Wprev_init, prm, workspace)
     return RunResult(o["Dn"], o["C"], o["I"], o["B_final"], o.get("B_hist"), keep)
+
+
+class RunGraph:
+    """A whole `run` captured once into a HIP graph (yuma_graph_create) and
+    replayed with one launch per call: the E-epoch loop of run_simulation
+    (simulation_utils.py:52-110) with no host work between phases or epochs.
+    Inputs and outputs are the buffers of the capture (`result`); refill the
+    inputs in place between replays."""
+
+    def __init__(self, variant: int, params: list[YumaParamsC], W: torch.Tensor, S: torch.Tensor,
+                 B_init: torch.Tensor | None = None, Wprev_init: torch.Tensor | None = None, **kw):
+        self._lib = load_library()
+        h: list = []
+        self.result = run(variant, params, W, S, B_init, Wprev_init, capture=h, **kw)
+        self._h = h[0]
+
+    def launch(self) -> RunResult:
+        stream = torch.cuda.current_stream(device()).cuda_stream
+        _check(self._lib.yuma_graph_launch(self._h, stream), "yuma_graph_launch")
+        return self.result
+
+    def nodes(self) -> int:
+        return int(self._lib.yuma_graph_nodes(self._h))
+
+    def close(self) -> None:
+        if self._h is not None:
+            self._lib.yuma_graph_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def shard_stage(stage: int, variant: int, prm: torch.Tensor, W: torch.Tensor, S: torch.Tensor,
