@@ -826,6 +826,86 @@ __global__ __launch_bounds__(256) void k_rank_w(
   }
 }
 
+// Clip + rank, streaming form for run outputs (no Wn / Wc / T_v, not Yuma2):
+// R[m] = sum_v S[v] min(W[v,m], C[m]) (yumas.py:439-442). Nothing is held
+// across rows, so the block takes the bond kernel's wide layout (a wave
+// instruction moves 4 rows x 256 contiguous bytes instead of 16 x 64) and
+// streams its rows in batches of 8 loads per lane. Order: rows g, g+16, ...
+// sequentially per lane, then the 4 row groups of a wave (xor 16, 32), then
+// the 4 waves in order.
+template <bool VEC>
+__global__ __launch_bounds__(256) void k_rank_s(const float* __restrict__ W,
+                                                const float* __restrict__ rsd,
+                                                const float* __restrict__ sn,
+                                                const float* __restrict__ C, int N, int V, int M,
+                                                long long slice0, int tiles,
+                                                float* __restrict__ Rout,
+                                                float* __restrict__ rpart) {
+  __shared__ float4 red[4][16];
+  const Lay L = lay();
+  const long long slice = slice0 + blockIdx.x / tiles;
+  const int tile = blockIdx.x % tiles;
+  const long long VM = (long long)V * M;
+  const int m = tile * kTileM + L.c4 * 4;
+  const float* Ws = W + slice * VM;
+  float Cc[4];
+  load4c<VEC>(C + slice * M, 0, 1, m, M, Cc);
+  float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  constexpr int B = 8;
+  for (int r0 = L.g; r0 < V; r0 += 16 * B) {
+    float w[B][4], d[B], s[B];
+#pragma unroll
+    for (int i = 0; i < B; ++i) {
+      const int rr = min(r0 + 16 * i, V - 1);
+      load4c<VEC>(Ws, rr, V, m, M, w[i]);
+      d[i] = rsd[slice * V + rr];
+      s[i] = sn[slice * V + rr];
+    }
+    bool slow = false;
+#pragma unroll
+    for (int i = 0; i < B; ++i) {
+      const RowDiv rdv = row_div(d[i]);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) w[i][c] = div_fast(w[i][c], rdv, slow);
+    }
+    if (__any(slow)) {  // rare: redo the batch with IEEE division (wave-uniform)
+#pragma unroll
+      for (int i = 0; i < B; ++i) {
+        const int rr = min(r0 + 16 * i, V - 1);
+        float x[4];
+        load4c<VEC>(Ws, rr, V, m, M, x);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) w[i][c] = x[c] / d[i];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < B; ++i) {
+      const bool live = r0 + 16 * i < V;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const float x = s[i] * vmin(w[i][c], Cc[c]);
+        acc[c] = live ? acc[c] + x : acc[c];
+      }
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < 4; ++c) acc[c] = sum_rowgroups(acc[c]);
+  if (L.lane < 16) red[L.wave][L.c4] = make_float4(acc[0], acc[1], acc[2], acc[3]);
+  __syncthreads();
+  if (L.wave == 0) {
+    // lane l: miner tile*64 + l
+    const float* rf = reinterpret_cast<const float*>(&red[0][0]);
+    float r = rf[L.lane];
+#pragma unroll
+    for (int w = 1; w < 4; ++w) r = r + rf[w * 64 + L.lane];
+    const int mg = tile * kTileM + L.lane;
+    if (mg < M) Rout[slice * M + mg] = r;
+    float t = mg < M ? r : 0.0f;
+    t = wave_sum(t);
+    if (L.lane == 0) rpart[slice * tiles + tile] = t;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Block-wide reductions with a fixed order (thread-sequential, wave butterfly,
 // waves in order).
@@ -2623,6 +2703,11 @@ void launch_rank(RowCfg rc, long long nblocks, hipStream_t st, const float* W, c
                  int V, int M, long long slice0, int tiles, float* R, float* rpart, float* Wn,
                  float* Wc, float* tvc, float* tvn) {
   const bool full = Wn != nullptr || Wc != nullptr || tvc != nullptr;
+  const char* rk = getenv("YUMA_RANK");  // YUMA_RANK=w: the register-resident kernel (A/B)
+  if (!full && !yuma2 && !(rk != nullptr && rk[0] == 'w')) {
+    YK_LAUNCH(yk::k_rank_s<VEC>, nblocks, 256, st, W, rsd, sn, C, N, V, M, slice0, tiles, R, rpart);
+    return;
+  }
   auto go = [&](auto kern) {
     YK_LAUNCH(kern, nblocks, 256, st, W, rsd, sn, C, Wprev_init, yuma2, N, V, M, slice0, tiles, R,
               rpart, Wn, Wc, tvc, tvn);
