@@ -2773,8 +2773,8 @@ void launch_bonds_colnorm(RowCfg rc, long long nblocks, hipStream_t st, const yk
 // inputs of the next kPrefetch epochs kept in flight.
 // YUMA_BONDS=p4|p8|p4nt|p8nt|p4v selects the prefetch depth / history store
 // policy / float4 incentive loads (A/B knob for tools/ab.sh). The default is
-// the measured best on MI355X: 4 epochs in flight, plain stores, per-column
-// incentive loads (float4 ones measured 10% slower: 1.92 vs 1.74 ms at c2).
+// the measured best on MI355X: 4 epochs in flight, plain stores, and the
+// incentive-load width chosen by whether the bond history is written.
 int bonds_knob() {
   static int knob = -1;
   if (knob < 0) {
@@ -2797,7 +2797,15 @@ void launch_bonds_elem(int R, long long nblocks, hipStream_t st, const yk::BondA
     case 2: YK_LAUNCH((yk::k_bonds_elem<VARIANT, 1, VEC, 4, true>), nblocks, 256, st, A); break;
     case 3: YK_LAUNCH((yk::k_bonds_elem<VARIANT, 1, VEC, 8, true>), nblocks, 256, st, A); break;
     case 4: YK_LAUNCH((yk::k_bonds_elem<VARIANT, 1, VEC, 4, false, VEC>), nblocks, 256, st, A); break;
-    default: YK_LAUNCH((yk::k_bonds_elem<VARIANT, 1, VEC, 4, false>), nblocks, 256, st, A); break;
+    default:
+      // measured (MI355X, c2 / c3): per-column incentive / bond_alpha loads
+      // are faster while the bond history is written (1.73 vs 1.92 ms),
+      // float4 ones without it (1.11 vs 1.28 ms at c2, 18.0 vs 26.8 ms at c3)
+      if (A.B_hist == nullptr)
+        YK_LAUNCH((yk::k_bonds_elem<VARIANT, 1, VEC, 4, false, VEC>), nblocks, 256, st, A);
+      else
+        YK_LAUNCH((yk::k_bonds_elem<VARIANT, 1, VEC, 4, false>), nblocks, 256, st, A);
+      break;
   }
 }
 
