@@ -106,6 +106,17 @@ __device__ __forceinline__ float div_fast(float a, const RowDiv& rd, bool& slow)
   slow |= !(rd.ok && ((aa >= 0x1p-60f && aa <= 0x1p60f) || a == 0.0f));
   return a == 0.0f ? q : q1;
 }
+// div_fast without the signed-zero fix-up: a = -0 yields +0 instead of -0.
+// For the consensus search and the rank sums only (a comparison with a
+// positive grid point, min with C >= 0 times S, added to a +0-seeded sum
+// cannot tell the two apart); saves a compare and a select per element.
+__device__ __forceinline__ float div_fast_nz(float a, const RowDiv& rd, bool& slow) {
+  const float q = a * rd.r;
+  const float e = fmaf(-rd.d, q, a);
+  const float aa = fabsf(a);
+  slow |= !(rd.ok && ((aa >= 0x1p-60f && aa <= 0x1p60f) || a == 0.0f));
+  return fmaf(e, rd.r, q);
+}
 // a / d exactly as IEEE: fast path, IEEE if outside the guard (used where a
 // per-element branch is cheap: the rare paths themselves)
 __device__ __forceinline__ float div_rn(float a, const RowDiv& rd) {
@@ -555,7 +566,7 @@ __device__ __forceinline__ float qsum4(float x) {
 }
 
 // Load + normalise this lane's R rows x 4 miners of a slice (branch-free).
-template <int R, bool VEC>
+template <int R, bool VEC, bool SIGNED0 = true>
 __device__ __forceinline__ void load_norm_w(const float* __restrict__ Ws, const float* rsd_s,
                                             const float* sn_s, int V, int M, int m, int rg,
                                             float (&wn)[R][4], float (&s)[R]) {
@@ -573,7 +584,8 @@ __device__ __forceinline__ void load_norm_w(const float* __restrict__ Ws, const 
   for (int i = 0; i < R; ++i) {
     const RowDiv rdv = row_div(d[i]);
 #pragma unroll
-    for (int c = 0; c < 4; ++c) wn[i][c] = div_fast(wn[i][c], rdv, slow);
+    for (int c = 0; c < 4; ++c)
+      wn[i][c] = SIGNED0 ? div_fast(wn[i][c], rdv, slow) : div_fast_nz(wn[i][c], rdv, slow);
   }
   if (__any(slow)) {  // rare: some operand outside the fast-division guard
 #pragma unroll
@@ -606,8 +618,8 @@ __global__ __launch_bounds__(256) void k_consensus_w(const float* __restrict__ W
   const int m = tile * kTileM + L.wave * 16 + L.cq * 4;
   if (tile * kTileM + L.wave * 16 >= M) return;  // whole wave past the last miner
   float wn[R][4], s[R];
-  load_norm_w<R, VEC>(W + slice * (long long)V * M, rsd + slice * V, sn + slice * V, V, M, m,
-                      L.rg, wn, s);
+  load_norm_w<R, VEC, false>(W + slice * (long long)V * M, rsd + slice * V, sn + slice * V, V, M,
+                             m, L.rg, wn, s);
   if (Pout != nullptr) {
     float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
@@ -866,7 +878,7 @@ __global__ __launch_bounds__(256) void k_rank_s(const float* __restrict__ W,
     for (int i = 0; i < B; ++i) {
       const RowDiv rdv = row_div(d[i]);
 #pragma unroll
-      for (int c = 0; c < 4; ++c) w[i][c] = div_fast(w[i][c], rdv, slow);
+      for (int c = 0; c < 4; ++c) w[i][c] = div_fast_nz(w[i][c], rdv, slow);
     }
     if (__any(slow)) {  // rare: redo the batch with IEEE division (wave-uniform)
 #pragma unroll
