@@ -444,3 +444,44 @@ def test_graph_replay_equals_direct_run(variant, chunk):
                      (r.B_final, ref.B_final)):
             assert torch.equal(a, b)
     g.close()
+
+
+@pytest.mark.parametrize("V,M,kind", [(256, 4096, "synth"), (64, 300, "randw"), (200, 130, "randw"),
+                                      (33, 65, "synth"), (256, 1024, "nan_inf")])
+def test_consensus_histogram_finish_equals_bisection(V, M, kind, monkeypatch):
+    """The exact-stake histogram finish of the consensus search (default) and
+    the plain bisection (YUMA_CHIST=0) give bitwise-equal consensus on inputs
+    whose stakes are multiples of 2^-24 (synth.stakes sums to 2^20), across
+    kappa / precision settings and bracket widths above the 64-bin limit
+    (random-float weights); and both match the oracle. The nan_inf kind puts
+    NaN / +inf / -inf / negative weights into some columns."""
+    E = 3
+    S = synth.stakes(0x5EEDC0 + V, E, 1, V, period=2)
+    if kind == "synth":
+        W = synth.weights(0x5EEDC0 + M, E, 1, V, M)
+    else:
+        rng = np.random.default_rng(V * 7 + M)
+        W = rng.random((E, 1, V, M), dtype=np.float32)
+        W[:, :, :, 0] = 0.0
+        if kind == "nan_inf":
+            W[0, 0, 3, 5] = np.nan
+            W[1, 0, 7, 9] = np.inf
+            W[1, 0, 8, 11] = -np.inf
+            W[2, 0, 1, 13] = -0.5
+    for spec in ({}, {"kappa": 0.3}, {"kappa": 0.7}, {"consensus_precision": 1000}, {"consensus_precision": 10000000}):
+        cfg = config_from(spec)
+        vid = engine.VARIANT_YUMA3
+        prm = [engine.make_params(vid, cfg)]
+        Wt, St = torch.from_numpy(W), torch.from_numpy(S)
+        monkeypatch.setenv("YUMA_CHIST", "1")
+        a = engine.run(vid, prm, Wt, St, want_hist=True)
+        monkeypatch.setenv("YUMA_CHIST", "0")
+        b = engine.run(vid, prm, Wt, St, want_hist=True)
+        torch.cuda.synchronize()
+        tag = f"{kind} {V}x{M} {spec}"
+        assert torch.equal(a.C, b.C), tag
+        bits = lambda t: t.contiguous().view(torch.int32)  # NaN-safe bitwise compare
+        assert torch.equal(bits(a.B_hist), bits(b.B_hist)) and torch.equal(bits(a.Dn), bits(b.Dn)), tag
+        if kind != "nan_inf":
+            ref = orc.run("Yuma 3 (Rhef)", W[:, 0], S[:, 0], cfg)
+            np.testing.assert_array_equal(a.C[:, 0].cpu().numpy(), ref["C"], err_msg=tag)

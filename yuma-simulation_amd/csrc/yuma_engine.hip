@@ -558,6 +558,24 @@ __device__ __forceinline__ float wmin16(float x) {
   x = fminf(x, dpp_f<0x140>(x));
   return x;
 }
+// Integer sum over the 16 lanes of a DPP row (exact, so any order).
+__device__ __forceinline__ int iwsum16(int x) {
+  x = x + __builtin_amdgcn_mov_dpp(x, 0xB1, 0xF, 0xF, false);
+  x = x + __builtin_amdgcn_mov_dpp(x, 0x4E, 0xF, 0xF, false);
+  x = x + __builtin_amdgcn_mov_dpp(x, 0x141, 0xF, 0xF, false);
+  x = x + __builtin_amdgcn_mov_dpp(x, 0x140, 0xF, 0xF, false);
+  return x;
+}
+// Exclusive prefix sum over the 16 lanes of a DPP row (row_shr:1,2,4,8 with
+// bound_ctrl: lanes shifted in from outside the row read 0).
+__device__ __forceinline__ int iscan16_excl(int x) {
+  int y = x;
+  y = y + __builtin_amdgcn_update_dpp(0, y, 0x111, 0xF, 0xF, true);
+  y = y + __builtin_amdgcn_update_dpp(0, y, 0x112, 0xF, 0xF, true);
+  y = y + __builtin_amdgcn_update_dpp(0, y, 0x114, 0xF, 0xF, true);
+  y = y + __builtin_amdgcn_update_dpp(0, y, 0x118, 0xF, 0xF, true);
+  return y - x;
+}
 // sum over the 4 column quads of a wave (lanes l, l^16, l^32, l^48)
 __device__ __forceinline__ float qsum4(float x) {
   x = x + __shfl_xor(x, 16, 64);
@@ -603,8 +621,11 @@ __device__ __forceinline__ void load_norm_w(const float* __restrict__ Ws, const 
 }
 
 // Consensus (see k_consensus for the search argument), wave-owned columns.
-template <int R, bool VEC>
-__global__ __launch_bounds__(256) void k_consensus_w(const float* __restrict__ W,
+// HIST: exact-stake histogram finish (below); kHB grid points per column,
+// kHS words per column in LDS (16-B aligned, 4-bank skew between columns).
+constexpr int kHB = 64, kHS = 68;
+template <int R, bool VEC, bool HIST>
+__global__ __launch_bounds__(256, 3) void k_consensus_w(const float* __restrict__ W,
                                                      const float* __restrict__ rsd,
                                                      const float* __restrict__ sn,
                                                      const yuma_params_t* __restrict__ prm, int N,
@@ -690,10 +711,45 @@ __global__ __launch_bounds__(256) void k_consensus_w(const float* __restrict__ W
       hi_k[c] = hi_c;
     }
   }
+  // Exact-stake finish (HIST): when every normalised stake is a multiple of
+  // 2^-24 and they total <= 1, every subset sum of stakes is exact in fp32,
+  // so F(k) = sum_v S[v]·[Wn[v,m] > k/2^iters] does not depend on summation
+  // order and equals the reference's fp32 sum. Then one stake histogram over
+  // the bracket's grid points (integer stake units, LDS integer atomics ->
+  // deterministic) answers the whole remaining search at once: the result of
+  // the bisection over [lo, hi] is lo + 1 + #{b in [1, w-1] : F(lo+b) > κ}
+  // (F is non-increasing). Brackets wider than kHB-1 grid points are first
+  // narrowed by ordinary bisection passes. Any other input (generic float
+  // stakes, non-finite or > 2 weights) takes the bisection unchanged.
+  int lim = 1;
+  bool hist = false;
+  int thr = 0;
+  if constexpr (HIST) {
+    bool ok = bracket;
+    int ut = 0;
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      // in double so the compiler keeps no fp32 copy of s·2^24 alive
+      // across the search (the histogram recomputes it)
+      const double f = (double)s[i] * 16777216.0;
+      ok &= f >= 0.0 && f <= 16777216.0 && f == rint(f);
+      ut += ok ? (int)f : 0;
+    }
+    ut = iwsum16(ut);
+    ok &= ut <= (1 << 24);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) ok &= hi_k[c] > lo_k[c];
+    hist = __all(ok);
+    if (hist) {
+      lim = kHB - 1;
+      const double kd = floor((double)kappa * 16777216.0);
+      thr = ut - (kd > 33554432.0 ? 33554432 : (int)kd);
+    }
+  }
   for (;;) {
     bool active = false;
 #pragma unroll
-    for (int c = 0; c < 4; ++c) active |= (hi_k[c] - lo_k[c]) > 1;
+    for (int c = 0; c < 4; ++c) active |= (hi_k[c] - lo_k[c]) > lim;
     if (!__any(active)) break;
     float part[4], midf[4];
     int mid[4];
@@ -712,9 +768,60 @@ __global__ __launch_bounds__(256) void k_consensus_w(const float* __restrict__ W
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       part[c] = wsum16(part[c]);
-      const bool act = hi_k[c] - lo_k[c] > 1, up = part[c] > kappa;
+      const bool act = hi_k[c] - lo_k[c] > lim, up = part[c] > kappa;
       lo_k[c] = (act && up) ? mid[c] : lo_k[c];
       hi_k[c] = (act && !up) ? mid[c] : hi_k[c];
+    }
+  }
+  if constexpr (HIST) {
+    if (hist) {
+      __shared__ __attribute__((aligned(16))) unsigned hb[4 * 16 * kHS];
+      unsigned* wb = hb + L.wave * 16 * kHS;  // this wave's 16 columns
+      uint4* wb4 = reinterpret_cast<uint4*>(wb);
+      for (int j = L.lane; j < 16 * kHS / 4; j += 64) wb4[j] = make_uint4(0u, 0u, 0u, 0u);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      unsigned su[R];  // stakes in units of 2^-24 (exact, checked above)
+#pragma unroll
+      for (int i = 0; i < R; ++i) su[i] = (unsigned)(s[i] * 16777216.0f);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        unsigned* cb = wb + (L.cq * 4 + c) * kHS;
+        const float nlo = -(float)lo_k[c];
+        const unsigned w = (unsigned)(hi_k[c] - lo_k[c]);
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+          // bin = clamp(ceil(wn·2^iters) - lo, 0, w). wn·2^iters is exact,
+          // and so is its difference with the integer lo whenever it is
+          // >= 0 (both are multiples of ulp(wn·2^iters)); anything that
+          // rounds is negative and lands in bin 0 either way. The u32
+          // convert saturates (negatives and -inf -> 0, +inf -> max) and
+          // maps NaN to 0, i.e. never above a grid point, as `>` does.
+          const unsigned k = (unsigned)ceilf(fmaf(wn[i][c], scale, nlo));
+          atomicAdd(cb + (k < w ? k : w), su[i]);
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const uint4 h = *reinterpret_cast<const uint4*>(wb + (L.cq * 4 + c) * kHS + 4 * L.rg);
+        int p[4];
+        p[0] = (int)h.x;
+        p[1] = p[0] + (int)h.y;
+        p[2] = p[1] + (int)h.z;
+        p[3] = p[2] + (int)h.w;
+        const int e = iscan16_excl(p[3]), w = hi_k[c] - lo_k[c];
+        int cnt = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int b = 4 * L.rg + j;
+          cnt += (b >= 1 && b < w && e + p[j] < thr) ? 1 : 0;
+        }
+        hi_k[c] = lo_k[c] + 1 + iwsum16(cnt);
+      }
     }
   }
   if (L.rg == 0)
@@ -2628,22 +2735,38 @@ RowCfg row_cfg(int V) {
 #define YK_LAUNCH(kernel, grid, block, stream, ...) \
   hipLaunchKernelGGL(kernel, dim3(grid), dim3(block), 0, (hipStream_t)(stream), __VA_ARGS__)
 
+// YUMA_CHIST=0 turns the exact-stake histogram finish of the consensus
+// search off (A/B knob); it is on by default.
+bool chist_knob() {
+  const char* e = getenv("YUMA_CHIST");  // read per launch: tests A/B in one process
+  return !(e != nullptr && !strcmp(e, "0"));
+}
+
+template <int R, bool VEC>
+void launch_consensus_w(long long nblocks, hipStream_t st, const float* W, const float* rsd,
+                        const float* sn, const yuma_params_t* prm, int N, int V, int M,
+                        long long slice0, int tiles, double* craw, float* P) {
+  if (chist_knob())
+    YK_LAUNCH((yk::k_consensus_w<R, VEC, true>), nblocks, 256, st, W, rsd, sn, prm, N, V, M,
+              slice0, tiles, craw, P);
+  else
+    YK_LAUNCH((yk::k_consensus_w<R, VEC, false>), nblocks, 256, st, W, rsd, sn, prm, N, V, M,
+              slice0, tiles, craw, P);
+}
+
 template <bool VEC>
 void launch_consensus(RowCfg rc, long long nblocks, hipStream_t st, const float* W,
                       const float* rsd, const float* sn, const yuma_params_t* prm, int N, int V,
                       int M, long long slice0, int tiles, double* craw, float* P) {
   switch (rc) {  // wave-owned columns up to 256 validators
     case RC_256_1:
-      YK_LAUNCH((yk::k_consensus_w<1, VEC>), nblocks, 256, st, W, rsd, sn, prm, N, V, M, slice0,
-                tiles, craw, P);
+      launch_consensus_w<1, VEC>(nblocks, st, W, rsd, sn, prm, N, V, M, slice0, tiles, craw, P);
       return;
     case RC_256_4:
-      YK_LAUNCH((yk::k_consensus_w<4, VEC>), nblocks, 256, st, W, rsd, sn, prm, N, V, M, slice0,
-                tiles, craw, P);
+      launch_consensus_w<4, VEC>(nblocks, st, W, rsd, sn, prm, N, V, M, slice0, tiles, craw, P);
       return;
     case RC_256_16:
-      YK_LAUNCH((yk::k_consensus_w<16, VEC>), nblocks, 256, st, W, rsd, sn, prm, N, V, M, slice0,
-                tiles, craw, P);
+      launch_consensus_w<16, VEC>(nblocks, st, W, rsd, sn, prm, N, V, M, slice0, tiles, craw, P);
       return;
     default:
       break;
