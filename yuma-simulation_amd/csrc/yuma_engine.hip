@@ -598,12 +598,46 @@ __device__ __forceinline__ void load_norm_w(const float* __restrict__ Ws, const 
     s[i] = sn_s[rr];
   }
   bool slow = false;
+  if constexpr (SIGNED0) {
 #pragma unroll
-  for (int i = 0; i < R; ++i) {
-    const RowDiv rdv = row_div(d[i]);
+    for (int i = 0; i < R; ++i) {
+      const RowDiv rdv = row_div(d[i]);
 #pragma unroll
-    for (int c = 0; c < 4; ++c)
-      wn[i][c] = SIGNED0 ? div_fast(wn[i][c], rdv, slow) : div_fast_nz(wn[i][c], rdv, slow);
+      for (int c = 0; c < 4; ++c) wn[i][c] = div_fast(wn[i][c], rdv, slow);
+    }
+  } else {
+    // div_fast_nz on packed pairs (v_pk_mul / v_pk_fma: two lanes' worth of
+    // fp32 per instruction), with the operand guard reduced to a lane-wide
+    // max |a| (NaN-ignoring: the fast path returns the same quiet NaN as
+    // IEEE division) and a min over nonzero |a| taken on 2·bits(|a|) - 1
+    // (zeros wrap to the maximum), instead of three compares per element.
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    float amax = 0.0f;
+    unsigned ymin = 0xFFFFFFFFu;
+    bool dok = true;
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const RowDiv rdv = row_div(d[i]);
+      dok &= rdv.ok;
+      const f2 r2 = {rdv.r, rdv.r}, nd2 = {-rdv.d, -rdv.d};
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const f2 a2 = {wn[i][2 * h], wn[i][2 * h + 1]};
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          amax = fmaxf(amax, fabsf(a2[c]));
+          const unsigned y = (__float_as_uint(a2[c]) << 1) - 1u;
+          ymin = y < ymin ? y : ymin;
+        }
+        const f2 q = a2 * r2;
+        const f2 e = __builtin_elementwise_fma(nd2, q, a2);
+        const f2 q1 = __builtin_elementwise_fma(e, r2, q);
+        wn[i][2 * h] = q1[0];
+        wn[i][2 * h + 1] = q1[1];
+      }
+    }
+    slow = !(dok && amax <= 0x1p60f &&
+             (ymin == 0xFFFFFFFFu || ymin + 1u >= (__float_as_uint(0x1p-60f) << 1)));
   }
   if (__any(slow)) {  // rare: some operand outside the fast-division guard
 #pragma unroll
@@ -613,10 +647,14 @@ __device__ __forceinline__ void load_norm_w(const float* __restrict__ Ws, const 
       for (int c = 0; c < 4; ++c) wn[i][c] = wn[i][c] / d[i];
     }
   }
+  // padding rows / columns: a wave-uniform branch, so full tiles pay nothing
+  const bool full = rg + 16 * (R - 1) < V && m + 3 < M;
+  if (!__all(full)) {
 #pragma unroll
-  for (int i = 0; i < R; ++i) {
-    mask4(rg + 16 * i, V, m, M, wn[i]);
-    if (rg + 16 * i >= V) s[i] = 0.0f;
+    for (int i = 0; i < R; ++i) {
+      mask4(rg + 16 * i, V, m, M, wn[i]);
+      if (rg + 16 * i >= V) s[i] = 0.0f;
+    }
   }
 }
 
