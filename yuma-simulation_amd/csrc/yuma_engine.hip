@@ -589,13 +589,35 @@ __device__ __forceinline__ void load_norm_w(const float* __restrict__ Ws, const 
                                             const float* sn_s, int V, int M, int m, int rg,
                                             float (&wn)[R][4], float (&s)[R]) {
   float d[R];
+  // padding rows / columns exist only in edge tiles (wave-uniform test)
+  const bool full = rg + 16 * (R - 1) < V && m + 3 < M;
+  const bool allfull = VEC && __all(full) && (long long)V * M < (1ll << 30);
+  if (allfull) {
+    // 32-bit element offsets from the uniform slice base (saddr + voffset
+    // loads, one add per row instead of a 64-bit address per row)
+    const unsigned o0 = (unsigned)rg * (unsigned)M + (unsigned)m, st = 16u * (unsigned)M;
 #pragma unroll
-  for (int i = 0; i < R; ++i) load4c<VEC>(Ws, rg + 16 * i, V, m, M, wn[i]);
+    for (int i = 0; i < R; ++i) {
+      const float4 t = *reinterpret_cast<const float4*>(Ws + (o0 + (unsigned)i * st));
+      wn[i][0] = t.x;
+      wn[i][1] = t.y;
+      wn[i][2] = t.z;
+      wn[i][3] = t.w;
+    }
 #pragma unroll
-  for (int i = 0; i < R; ++i) {
-    const int rr = min(rg + 16 * i, V - 1);
-    d[i] = rsd_s[rr];
-    s[i] = sn_s[rr];
+    for (int i = 0; i < R; ++i) {
+      d[i] = rsd_s[rg + 16 * i];
+      s[i] = sn_s[rg + 16 * i];
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < R; ++i) load4c<VEC>(Ws, rg + 16 * i, V, m, M, wn[i]);
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const int rr = min(rg + 16 * i, V - 1);
+      d[i] = rsd_s[rr];
+      s[i] = sn_s[rr];
+    }
   }
   bool slow = false;
   if constexpr (SIGNED0) {
@@ -612,14 +634,17 @@ __device__ __forceinline__ void load_norm_w(const float* __restrict__ Ws, const 
     // IEEE division) and a min over nonzero |a| taken on 2·bits(|a|) - 1
     // (zeros wrap to the maximum), instead of three compares per element.
     typedef float f2 __attribute__((ext_vector_type(2)));
-    float amax = 0.0f;
+    float amax = 0.0f, dmin = INFINITY;
     unsigned ymin = 0xFFFFFFFFu;
-    bool dok = true;
+    // The four DPP rows of a wave hold the same 16·R validator rows, so each
+    // lane computes the IEEE reciprocal of R/4 of them (row 4j + cq) and
+    // the rest arrive by ds_bpermute from lane rg + 16·(i & 3).
 #pragma unroll
     for (int i = 0; i < R; ++i) {
-      const RowDiv rdv = row_div(d[i]);
-      dok &= rdv.ok;
-      const f2 r2 = {rdv.r, rdv.r}, nd2 = {-rdv.d, -rdv.d};
+      const float r = 1.0f / d[i];
+      amax = fmaxf(amax, fabsf(d[i]));
+      dmin = fminf(dmin, fabsf(d[i]));
+      const f2 r2 = {r, r}, nd2 = {-d[i], -d[i]};
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const f2 a2 = {wn[i][2 * h], wn[i][2 * h + 1]};
@@ -636,7 +661,7 @@ __device__ __forceinline__ void load_norm_w(const float* __restrict__ Ws, const 
         wn[i][2 * h + 1] = q1[1];
       }
     }
-    slow = !(dok && amax <= 0x1p60f &&
+    slow = !(dmin >= 0x1p-60f && amax <= 0x1p60f &&
              (ymin == 0xFFFFFFFFu || ymin + 1u >= (__float_as_uint(0x1p-60f) << 1)));
   }
   if (__any(slow)) {  // rare: some operand outside the fast-division guard
@@ -647,8 +672,6 @@ __device__ __forceinline__ void load_norm_w(const float* __restrict__ Ws, const 
       for (int c = 0; c < 4; ++c) wn[i][c] = wn[i][c] / d[i];
     }
   }
-  // padding rows / columns: a wave-uniform branch, so full tiles pay nothing
-  const bool full = rg + 16 * (R - 1) < V && m + 3 < M;
   if (!__all(full)) {
 #pragma unroll
     for (int i = 0; i < R; ++i) {
@@ -680,11 +703,18 @@ __global__ __launch_bounds__(256, 3) void k_consensus_w(const float* __restrict_
   load_norm_w<R, VEC, false>(W + slice * (long long)V * M, rsd + slice * V, sn + slice * V, V, M,
                              m, L.rg, wn, s);
   if (Pout != nullptr) {
-    float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    // P = sum_v S·Wn (yumas.py:192): product rounded, then summed (no FMA),
+    // two columns per packed v_pk_mul / v_pk_add
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    f2 a01 = {0.0f, 0.0f}, a23 = {0.0f, 0.0f};
 #pragma unroll
-    for (int i = 0; i < R; ++i)
-#pragma unroll
-      for (int c = 0; c < 4; ++c) acc[c] = acc[c] + s[i] * wn[i][c];
+    for (int i = 0; i < R; ++i) {
+      const f2 s2 = {s[i], s[i]};
+      const f2 w01 = {wn[i][0], wn[i][1]}, w23 = {wn[i][2], wn[i][3]};
+      a01 = a01 + s2 * w01;
+      a23 = a23 + s2 * w23;
+    }
+    float acc[4] = {a01[0], a01[1], a23[0], a23[1]};
 #pragma unroll
     for (int c = 0; c < 4; ++c) acc[c] = wsum16(acc[c]);
     if (L.rg == 0)
@@ -767,11 +797,12 @@ __global__ __launch_bounds__(256, 3) void k_consensus_w(const float* __restrict_
     int ut = 0;
 #pragma unroll
     for (int i = 0; i < R; ++i) {
-      // in double so the compiler keeps no fp32 copy of s·2^24 alive
-      // across the search (the histogram recomputes it)
-      const double f = (double)s[i] * 16777216.0;
-      ok &= f >= 0.0 && f <= 16777216.0 && f == rint(f);
-      ut += ok ? (int)f : 0;
+      // ldexp here, a multiply in the histogram: the compiler keeps no
+      // fp32 copy of s·2^24 alive across the search. s >= 0 and finite
+      // (bracket), so s·2^24 is an integer iff its fraction is 0.
+      const float f = ldexpf(s[i], 24);
+      ok &= f <= 16777216.0f && __builtin_amdgcn_fractf(f) == 0.0f;
+      ut += (int)f;
     }
     ut = iwsum16(ut);
     ok &= ut <= (1 << 24);
