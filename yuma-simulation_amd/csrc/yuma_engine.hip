@@ -32,6 +32,7 @@
 #include <hip/hip_runtime.h>
 
 #include <float.h>
+#include <limits.h>
 #include <math.h>
 #include <stdarg.h>
 #include <stdint.h>
@@ -566,6 +567,20 @@ __device__ __forceinline__ int iwsum16(int x) {
   x = x + __builtin_amdgcn_mov_dpp(x, 0x140, 0xF, 0xF, false);
   return x;
 }
+__device__ __forceinline__ int iwmax16(int x) {
+  x = max(x, __builtin_amdgcn_mov_dpp(x, 0xB1, 0xF, 0xF, false));
+  x = max(x, __builtin_amdgcn_mov_dpp(x, 0x4E, 0xF, 0xF, false));
+  x = max(x, __builtin_amdgcn_mov_dpp(x, 0x141, 0xF, 0xF, false));
+  x = max(x, __builtin_amdgcn_mov_dpp(x, 0x140, 0xF, 0xF, false));
+  return x;
+}
+__device__ __forceinline__ int iwmin16(int x) {
+  x = min(x, __builtin_amdgcn_mov_dpp(x, 0xB1, 0xF, 0xF, false));
+  x = min(x, __builtin_amdgcn_mov_dpp(x, 0x4E, 0xF, 0xF, false));
+  x = min(x, __builtin_amdgcn_mov_dpp(x, 0x141, 0xF, 0xF, false));
+  x = min(x, __builtin_amdgcn_mov_dpp(x, 0x140, 0xF, 0xF, false));
+  return x;
+}
 // Exclusive prefix sum over the 16 lanes of a DPP row (row_shr:1,2,4,8 with
 // bound_ctrl: lanes shifted in from outside the row read 0).
 __device__ __forceinline__ int iscan16_excl(int x) {
@@ -738,30 +753,41 @@ __global__ __launch_bounds__(256, 3) void k_consensus_w(const float* __restrict_
     hi_k[c] = top;
   }
   if (bracket) {
-    float vmax[4], vmin[4], stot = 0.0f;
+    // Column max / min on the fp32 bit patterns as signed integers (the
+    // order of non-negative floats; negatives, -0 and negative NaNs compare
+    // below +0): v_max3_i32 / v_min3_i32 with no NaN canonicalisation. A
+    // positive NaN shows up as a max above +inf and drops that column's
+    // bracket (the search then starts from [0, 2^iters]); clamping the min
+    // at +0 afterwards equals the min of max(wn, 0). Padding rows hold
+    // wn = 0, s = 0 (only lowers the min: a wider, still valid bracket).
+    int imax[4], imin[4];
+    float stot = 0.0f;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-      vmax[c] = -INFINITY;
-      vmin[c] = INFINITY;
+      imax[c] = INT_MIN;
+      imin[c] = INT_MAX;
     }
 #pragma unroll
     for (int i = 0; i < R; ++i) {
-      if (L.rg + 16 * i >= V) continue;
       stot = stot + s[i];
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
-        // NaN-ignoring max (v_max3 pairs); NaN and negatives count as 0 for
-        // the min: gmin below only asks whether it is > 0
-        vmax[c] = fmaxf(vmax[c], wn[i][c]);
-        vmin[c] = fminf(vmin[c], fmaxf(wn[i][c], 0.0f));
+        const int b = __float_as_int(wn[i][c]);
+        imax[c] = b > imax[c] ? b : imax[c];
+        imin[c] = b < imin[c] ? b : imin[c];
       }
     }
     // F(k) with every mask set, in exactly the order every F below uses
     stot = wsum16(stot);
+    float vmax[4], vmin[4];
+    bool nanc[4];
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-      vmax[c] = wmax16(vmax[c]);
-      vmin[c] = wmin16(vmin[c]);
+      imax[c] = iwmax16(imax[c]);
+      imin[c] = iwmin16(imin[c]);
+      nanc[c] = imax[c] > 0x7f800000;
+      vmax[c] = __int_as_float(imax[c]);
+      vmin[c] = imin[c] > 0 ? __int_as_float(imin[c]) : 0.0f;
       const int gmax = vmax[c] > 0.0f ? (int)fminf(ceilf(vmax[c] * scale), scale) : 0;
       const int gmin = vmin[c] > 0.0f ? (int)fminf(ceilf(vmin[c] * scale), scale + 1.0f) : 0;
       int lo_c = gmin >= 2 ? gmin - 1 : 0;
@@ -775,8 +801,8 @@ __global__ __launch_bounds__(256, 3) void k_consensus_w(const float* __restrict_
         hi_c = top;
       }
       if (hi_c <= lo_c) hi_c = lo_c + 1;
-      lo_k[c] = lo_c;
-      hi_k[c] = hi_c;
+      lo_k[c] = nanc[c] ? 0 : lo_c;
+      hi_k[c] = nanc[c] ? top : hi_c;
     }
   }
   // Exact-stake finish (HIST): when every normalised stake is a multiple of
