@@ -297,7 +297,7 @@ __global__ __launch_bounds__(256) void k_rowsum(const float* __restrict__ W,
                                                 const float* __restrict__ S, int V, int M,
                                                 long long slice0, int rowblocks,
                                                 float* __restrict__ rsd, float* __restrict__ sn,
-                                                int partial) {
+                                                int partial, int* __restrict__ sx) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const long long slice = slice0 + blockIdx.x / rowblocks;
   const int rb = blockIdx.x % rowblocks;
@@ -326,7 +326,21 @@ __global__ __launch_bounds__(256) void k_rowsum(const float* __restrict__ W,
     float acc = 0.0f;
     for (int v = lane; v < V; v += 64) acc = acc + s[v];
     acc = wave_sum(acc);
-    for (int v = lane; v < V; v += 64) sn[slice * V + v] = s[v] / acc;
+    // sx[slice]: the normalised stakes in units of 2^-24 when every one is
+    // such a multiple and they total <= 1 (subset sums exact in fp32: the
+    // consensus search's histogram finish), else -1
+    int units = 0;
+    bool exact = true;
+    for (int v = lane; v < V; v += 64) {
+      const float q = s[v] / acc;
+      sn[slice * V + v] = q;
+      const float f = q * 16777216.0f;
+      exact &= f >= 0.0f && f <= 16777216.0f && __builtin_amdgcn_fractf(f) == 0.0f;
+      units += exact ? (int)f : 0;
+    }
+    for (int o = 1; o < 64; o <<= 1) units += __shfl_xor(units, o, 64);
+    exact = __all(exact) && units <= (1 << 24);
+    if (lane == 0) sx[slice] = exact ? units : -1;
   }
 }
 
@@ -704,6 +718,7 @@ template <int R, bool VEC, bool HIST>
 __global__ __launch_bounds__(256, 3) void k_consensus_w(const float* __restrict__ W,
                                                      const float* __restrict__ rsd,
                                                      const float* __restrict__ sn,
+                                                     const int* __restrict__ sx,
                                                      const yuma_params_t* __restrict__ prm, int N,
                                                      int V, int M, long long slice0, int tiles,
                                                      double* __restrict__ craw,
@@ -819,22 +834,9 @@ __global__ __launch_bounds__(256, 3) void k_consensus_w(const float* __restrict_
   bool hist = false;
   int thr = 0;
   if constexpr (HIST) {
-    bool ok = bracket;
-    int ut = 0;
-#pragma unroll
-    for (int i = 0; i < R; ++i) {
-      // ldexp here, a multiply in the histogram: the compiler keeps no
-      // fp32 copy of s·2^24 alive across the search. s >= 0 and finite
-      // (bracket), so s·2^24 is an integer iff its fraction is 0.
-      const float f = ldexpf(s[i], 24);
-      ok &= f <= 16777216.0f && __builtin_amdgcn_fractf(f) == 0.0f;
-      ut += (int)f;
-    }
-    ut = iwsum16(ut);
-    ok &= ut <= (1 << 24);
-#pragma unroll
-    for (int c = 0; c < 4; ++c) ok &= hi_k[c] > lo_k[c];
-    hist = __all(ok);
+    // slice-uniform: k_rowsum checked the stakes (sx = exact units or -1)
+    const int ut = sx[slice];
+    hist = bracket && ut >= 0;
     if (hist) {
       lim = kHB - 1;
       const double kd = floor((double)kappa * 16777216.0);
@@ -2750,6 +2752,7 @@ size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
 struct Workspace {
   float* rsd;
+  int* sx;  // per slice: exact stake units or -1 (k_rowsum)
   float* sn;
   double* craw;
   int* qlev;
@@ -2789,6 +2792,7 @@ Workspace carve(char* base, int variant, int N, int E, int V, int M, int full) {
     return p;
   };
   w.rsd = (float*)take(S * V * 4);
+  w.sx = (int*)take(S * 4);
   w.sn = (float*)take(S * V * 4);
   w.craw = (double*)take(S * M * 8);
   w.qlev = (int*)take(S * M * 4);
@@ -2839,29 +2843,33 @@ bool chist_knob() {
 
 template <int R, bool VEC>
 void launch_consensus_w(long long nblocks, hipStream_t st, const float* W, const float* rsd,
-                        const float* sn, const yuma_params_t* prm, int N, int V, int M,
-                        long long slice0, int tiles, double* craw, float* P) {
+                        const float* sn, const int* sx, const yuma_params_t* prm, int N, int V,
+                        int M, long long slice0, int tiles, double* craw, float* P) {
   if (chist_knob())
-    YK_LAUNCH((yk::k_consensus_w<R, VEC, true>), nblocks, 256, st, W, rsd, sn, prm, N, V, M,
+    YK_LAUNCH((yk::k_consensus_w<R, VEC, true>), nblocks, 256, st, W, rsd, sn, sx, prm, N, V, M,
               slice0, tiles, craw, P);
   else
-    YK_LAUNCH((yk::k_consensus_w<R, VEC, false>), nblocks, 256, st, W, rsd, sn, prm, N, V, M,
-              slice0, tiles, craw, P);
+    YK_LAUNCH((yk::k_consensus_w<R, VEC, false>), nblocks, 256, st, W, rsd, sn, sx, prm, N, V,
+              M, slice0, tiles, craw, P);
 }
 
 template <bool VEC>
 void launch_consensus(RowCfg rc, long long nblocks, hipStream_t st, const float* W,
-                      const float* rsd, const float* sn, const yuma_params_t* prm, int N, int V,
-                      int M, long long slice0, int tiles, double* craw, float* P) {
+                      const float* rsd, const float* sn, const int* sx,
+                      const yuma_params_t* prm, int N, int V, int M, long long slice0, int tiles,
+                      double* craw, float* P) {
   switch (rc) {  // wave-owned columns up to 256 validators
     case RC_256_1:
-      launch_consensus_w<1, VEC>(nblocks, st, W, rsd, sn, prm, N, V, M, slice0, tiles, craw, P);
+      launch_consensus_w<1, VEC>(nblocks, st, W, rsd, sn, sx, prm, N, V, M, slice0, tiles, craw,
+                                  P);
       return;
     case RC_256_4:
-      launch_consensus_w<4, VEC>(nblocks, st, W, rsd, sn, prm, N, V, M, slice0, tiles, craw, P);
+      launch_consensus_w<4, VEC>(nblocks, st, W, rsd, sn, sx, prm, N, V, M, slice0, tiles, craw,
+                                  P);
       return;
     case RC_256_16:
-      launch_consensus_w<16, VEC>(nblocks, st, W, rsd, sn, prm, N, V, M, slice0, tiles, craw, P);
+      launch_consensus_w<16, VEC>(nblocks, st, W, rsd, sn, sx, prm, N, V, M, slice0, tiles, craw,
+                                  P);
       return;
     default:
       break;
@@ -3287,16 +3295,16 @@ int run_impl(int variant, const yuma_params_t* prm, int N, int E, int V, int M, 
     tm.mark(0);
     if (vec)
       YK_LAUNCH(yk::k_rowsum<true>, ns * rowblocks4, 256, st, W, S, V, M, s0, rowblocks4,
-                ws.rsd, ws.sn, 0);
+                ws.rsd, ws.sn, 0, ws.sx);
     else
       YK_LAUNCH(yk::k_rowsum<false>, ns * rowblocks4, 256, st, W, S, V, M, s0, rowblocks4,
-                ws.rsd, ws.sn, 0);
+                ws.rsd, ws.sn, 0, ws.sx);
     tm.mark(1);
     if (vec)
-      launch_consensus<true>(rc, ns * tiles, st, W, ws.rsd, ws.sn, prm, N, V, M, s0, tiles,
+      launch_consensus<true>(rc, ns * tiles, st, W, ws.rsd, ws.sn, ws.sx, prm, N, V, M, s0, tiles,
                              ws.craw, out->P);
     else
-      launch_consensus<false>(rc, ns * tiles, st, W, ws.rsd, ws.sn, prm, N, V, M, s0, tiles,
+      launch_consensus<false>(rc, ns * tiles, st, W, ws.rsd, ws.sn, ws.sx, prm, N, V, M, s0, tiles,
                               ws.craw, out->P);
     tm.mark(2);
     YK_LAUNCH(yk::k_quantise<256>, ns, 256, st, ws.craw, prm, variant, N, M, s0, C, ws.qlev,
@@ -3437,10 +3445,10 @@ int shard_stage_impl(int stage, int variant, const yuma_params_t* prm, int N, in
       const int rb4 = (V + 3) / 4;
       if (vec)
         YK_LAUNCH(yk::k_rowsum<true>, ns * rb4, 256, st, W, S, V, M, 0LL, rb4, io->rowsum_part,
-                  ws.sn, 1);
+                  ws.sn, 1, ws.sx);
       else
         YK_LAUNCH(yk::k_rowsum<false>, ns * rb4, 256, st, W, S, V, M, 0LL, rb4, io->rowsum_part,
-                  ws.sn, 1);
+                  ws.sn, 1, ws.sx);
       break;
     }
     case 2: {
@@ -3450,10 +3458,10 @@ int shard_stage_impl(int stage, int variant, const yuma_params_t* prm, int N, in
       if (nb > 4096) nb = 4096;
       YK_LAUNCH(yk::k_add_eps, nb, 256, st, io->rowsum, ns * V, ws.rsd);
       if (vec)
-        launch_consensus<true>(rc, ns * tiles, st, W, ws.rsd, ws.sn, prm, N, V, M, 0LL, tiles,
+        launch_consensus<true>(rc, ns * tiles, st, W, ws.rsd, ws.sn, ws.sx, prm, N, V, M, 0LL, tiles,
                                ws.craw, out->P);
       else
-        launch_consensus<false>(rc, ns * tiles, st, W, ws.rsd, ws.sn, prm, N, V, M, 0LL, tiles,
+        launch_consensus<false>(rc, ns * tiles, st, W, ws.rsd, ws.sn, ws.sx, prm, N, V, M, 0LL, tiles,
                                 ws.craw, out->P);
       YK_LAUNCH(yk::k_csum, ns, 256, st, ws.craw, rust ? 1 : 0, M, io->csum_part, io->csum_part_d);
       break;
