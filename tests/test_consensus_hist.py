@@ -79,7 +79,10 @@ def hist_consensus(Wn: np.ndarray, S: np.ndarray, kappa: float, iters: int) -> n
         H = np.bincount(b[:, m], weights=units, minlength=KHB).astype(np.int64)
         P = np.cumsum(H)
         cnt = sum(1 for j in range(1, w[m]) if P[j] < ut - kk)
-        out[m] = lo[m] + 1 + cnt
+        # the kernel's form: B = #{b in [0, 64) : P(b) < thr}, lo + max(B, 1)
+        B = int(np.count_nonzero(P[:KHB] < ut - kk))
+        assert max(B, 1) == 1 + cnt
+        out[m] = lo[m] + max(B, 1)
     return out.astype(np.float64) / top
 
 

@@ -910,14 +910,14 @@ __global__ __launch_bounds__(256, 3) void k_consensus_w(const float* __restrict_
         p[1] = p[0] + (int)h.y;
         p[2] = p[1] + (int)h.z;
         p[3] = p[2] + (int)h.w;
-        const int e = iscan16_excl(p[3]), w = hi_k[c] - lo_k[c];
+        // P(b) is non-decreasing, so {b : P(b) < thr} is a prefix [0, B);
+        // bins b >= w hold P = total >= thr (κ >= 0), so B <= w and the
+        // count over [1, w-1] is max(B - 1, 0) without per-bin range tests
+        const int t = thr - iscan16_excl(p[3]);
         int cnt = 0;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int b = 4 * L.rg + j;
-          cnt += (b >= 1 && b < w && e + p[j] < thr) ? 1 : 0;
-        }
-        hi_k[c] = lo_k[c] + 1 + iwsum16(cnt);
+        for (int j = 0; j < 4; ++j) cnt += p[j] < t ? 1 : 0;
+        hi_k[c] = lo_k[c] + max(iwsum16(cnt), 1);
       }
     }
   }
