@@ -60,7 +60,8 @@ def phase_bytes(phase: str, V: int, M: int, variant: int, liquid: bool, hist: bo
                   + (4 * VM if hist else 0) + 4 * V * tiles + 8 * VM / max(chunk, 1)),
         "finalize": 4 * V * tiles + 4 * V + 4 * V,
         # one W read; writes rs, S/sum S, C_raw (f64), C, levels, R, tile sums
-        "phase1_fused": 4 * VM + 4 * V + 8 * V + 8 * M + 4 * M + 4 * M + 4 * M + 4 * tiles,
+        # one W read; S read; writes rs, S/sum S, C, levels, R, tile sums
+        "fused1": 4 * VM + 4 * V + 8 * V + 4 * M + 4 * M + 4 * M + 4 * ((M + 31) // 32),
         "liquid": (4 * M + 4 * M + 4 * M) if liquid else 8 * M,
     }
     return float(table[phase])

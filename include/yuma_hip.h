@@ -62,6 +62,11 @@ enum yuma_liquid_mode {
 
 enum yuma_override_flags { YUMA_OVR_HIGH = 1, YUMA_OVR_LOW = 2, YUMA_OVR_FORCE_Q99 = 4 };
 
+/* yuma_params_t.flags. YUMA_FLAG_NO_HIST: run the consensus search as the
+ * plain bisection even where the exact-stake histogram finish applies (both
+ * give the same result; tests compare them). */
+enum yuma_flags { YUMA_FLAG_NO_HIST = 1 };
+
 /* Per-scenario parameters: the flattened YumaConfig (yumas.py:7-45) with every
  * Python-double constant pre-rounded exactly as the reference's torch ops round
  * them (python scalars meet fp32 tensors as fp32). 128 bytes, naturally aligned. */
@@ -73,7 +78,7 @@ typedef struct yuma_params {
   int32_t reset_mode;       /* yuma_reset_mode                                     */
   int32_t reset_epoch;      /* epoch index of the reset (run_simulation epoch)     */
   int32_t reset_index;      /* miner column to reset                               */
-  int32_t reserved0;
+  int32_t flags;            /* yuma_flags (test switches; 0 in production)         */
   float kappa;              /* fp32(kappa)                                         */
   float bond_penalty;       /* fp32(beta)                                          */
   float one_minus_bond_penalty; /* fp32(1 - beta), difference taken in double      */
@@ -173,7 +178,7 @@ enum yuma_phase {
   YUMA_PHASE_INCENTIVE = 4, /* k_incentive: incentive, trust                    */
   YUMA_PHASE_BONDS = 5,     /* k_bonds:     bond recurrence over the chunk      */
   YUMA_PHASE_FINALIZE = 6,  /* k_finalize:  dividends                           */
-  YUMA_PHASE_FUSED1 = 7,    /* k_phase1:    phases 0,1,2(levels),3 in one W pass  */
+  YUMA_PHASE_FUSED1 = 7,    /* k_fused1:    phases 0,1,2(levels),3 in one W pass  */
   YUMA_PHASE_LIQUID = 8,    /* k_liquid:    liquid-alpha quantiles (fused path)   */
   YUMA_NUM_PHASES = 9
 };
@@ -253,6 +258,23 @@ int yuma_shard_stage(int stage, int variant, const yuma_params_t* params_dev, in
  * Bit-identical to yuma_simulation._internal.synth.weights (numpy).          */
 int yuma_synth_weights(uint64_t seed, int E, int N, int V, int M, int t0, float* W,
                        void* stream);
+
+/* Phase-1 path selection for this process (tests and A/B runs):
+ * YUMA_PATH_AUTO (default) and YUMA_PATH_MULTIPASS run the multi-pass
+ * kernels; YUMA_PATH_FUSED runs the single-read fused phase 1 (k_fused1)
+ * wherever it applies (run outputs, 32 <= V <= 256, M % 4 == 0, M >= 256,
+ * not Yuma2; measured slower at c2, kept for its experiments). Returns the
+ * previous setting. Not thread-safe against concurrent launches.          */
+enum yuma_path { YUMA_PATH_AUTO = 0, YUMA_PATH_MULTIPASS = 1, YUMA_PATH_FUSED = 2 };
+int yuma_set_path(int path);
+
+/* Synchronous check of a workspace after a run has completed: 0 = clean,
+ * 1 = a fused-phase-1 hand-off timed out (results invalid; a co-residency
+ * failure, never expected on an idle device), < 0 = error.                 */
+int yuma_workspace_status(const void* workspace);
+/* Diagnostics after a completed run: out4 = {status, -, fused-phase-1 sweeps
+ * that found their granule not yet published, polls they spent}.          */
+int yuma_workspace_counters(const void* workspace, unsigned* out4);
 
 const char* yuma_last_error(void);
 const char* yuma_version(void);

@@ -40,7 +40,6 @@
 #include <stdlib.h>
 #include <string.h>
 
-#include <mutex>
 #include <vector>
 
 #include "yuma_hip.h"
@@ -291,6 +290,11 @@ __device__ __forceinline__ void load4_vec(const float* __restrict__ v, int m, in
 // ---------------------------------------------------------------------------
 // Phase 1a: row sums (yumas.py:186 `W.sum(dim=1) + 1e-6`) and S / S.sum()
 // (yumas.py:189). One wave per row. Block x: (slice, 4-row block).
+// Summation order (shared with k_fused1, so both paths give the same bits):
+// the row is cut into 256-miner chunks; a chunk's partial is the balanced
+// binary tree over its 64 column quads of the sequential quad sums
+// ((x0+x1)+x2)+x3 (lane l holds quad l: the 64-lane butterfly); the chunk
+// partials are added in chunk order.
 // ---------------------------------------------------------------------------
 template <bool VEC>
 __global__ __launch_bounds__(256) void k_rowsum(const float* __restrict__ W,
@@ -305,19 +309,27 @@ __global__ __launch_bounds__(256) void k_rowsum(const float* __restrict__ W,
   if (row < V) {
     const float* r = W + (slice * V + row) * (long long)M;
     float acc = 0.0f;
-    if (VEC) {
-#pragma unroll 8
-      for (int m = lane * 4; m < M; m += 256) {
-        const float4 t = *reinterpret_cast<const float4*>(r + m);
-        acc = acc + t.x;
-        acc = acc + t.y;
-        acc = acc + t.z;
-        acc = acc + t.w;
+    for (int m0 = 0; m0 < M; m0 += 256) {
+      const int m = m0 + lane * 4;
+      float x[4];
+      if (VEC) {
+        if (m < M) {
+          const float4 t = *reinterpret_cast<const float4*>(r + m);
+          x[0] = t.x;
+          x[1] = t.y;
+          x[2] = t.z;
+          x[3] = t.w;
+        } else {
+          x[0] = x[1] = x[2] = x[3] = 0.0f;
+        }
+      } else {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) x[c] = m + c < M ? r[m + c] : 0.0f;
       }
-    } else {
-      for (int m = lane; m < M; m += 64) acc = acc + r[m];
+      float q = ((x[0] + x[1]) + x[2]) + x[3];
+      q = wave_sum(q);  // the balanced tree over the chunk's 64 quads
+      acc = acc + q;
     }
-    acc = wave_sum(acc);
     // partial (column shard): the caller sums the shards, then k_add_eps
     if (lane == 0) rsd[slice * V + row] = partial ? acc : acc + 1e-6f;
   }
@@ -710,50 +722,89 @@ __device__ __forceinline__ void load_norm_w(const float* __restrict__ Ws, const 
   }
 }
 
+// P = sum_v S·Wn (yumas.py:192) for this lane's 4 columns: product rounded,
+// then summed (no FMA), two columns per packed v_pk_mul / v_pk_add; row
+// order rg + 16 i per lane, then the 16-lane DPP tree.
+template <int R>
+__device__ __forceinline__ void prerank_store(const float (&wn)[R][4], const float (&s)[R],
+                                              const WLay& L, int m, int M, float* __restrict__ Pout) {
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  f2 a01 = {0.0f, 0.0f}, a23 = {0.0f, 0.0f};
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    const f2 s2 = {s[i], s[i]};
+    const f2 w01 = {wn[i][0], wn[i][1]}, w23 = {wn[i][2], wn[i][3]};
+    a01 = a01 + s2 * w01;
+    a23 = a23 + s2 * w23;
+  }
+  float acc[4] = {a01[0], a01[1], a23[0], a23[1]};
+#pragma unroll
+  for (int c = 0; c < 4; ++c) acc[c] = wsum16(acc[c]);
+  if (L.rg == 0)
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      if (m + c < M) Pout[m + c] = acc[c];
+}
+
 // Consensus (see k_consensus for the search argument), wave-owned columns.
 // HIST: exact-stake histogram finish (below); kHB grid points per column,
 // kHS words per column in LDS (16-B aligned, 4-bank skew between columns).
 constexpr int kHB = 64, kHS = 68;
-template <int R, bool VEC, bool HIST>
-__global__ __launch_bounds__(256, 3) void k_consensus_w(const float* __restrict__ W,
-                                                     const float* __restrict__ rsd,
-                                                     const float* __restrict__ sn,
-                                                     const int* __restrict__ sx,
-                                                     const yuma_params_t* __restrict__ prm, int N,
-                                                     int V, int M, long long slice0, int tiles,
-                                                     double* __restrict__ craw,
-                                                     float* __restrict__ Pout) {
-  const WLay L = wlay();
-  const long long slice = slice0 + blockIdx.x / tiles;
-  const int tile = blockIdx.x % tiles;
-  const int n = (int)(slice % N);
-  const int m = tile * kTileM + L.wave * 16 + L.cq * 4;
-  if (tile * kTileM + L.wave * 16 >= M) return;  // whole wave past the last miner
-  float wn[R][4], s[R];
-  load_norm_w<R, VEC, false>(W + slice * (long long)V * M, rsd + slice * V, sn + slice * V, V, M,
-                             m, L.rg, wn, s);
-  if (Pout != nullptr) {
-    // P = sum_v S·Wn (yumas.py:192): product rounded, then summed (no FMA),
-    // two columns per packed v_pk_mul / v_pk_add
-    typedef float f2 __attribute__((ext_vector_type(2)));
-    f2 a01 = {0.0f, 0.0f}, a23 = {0.0f, 0.0f};
-#pragma unroll
-    for (int i = 0; i < R; ++i) {
-      const f2 s2 = {s[i], s[i]};
-      const f2 w01 = {wn[i][0], wn[i][1]}, w23 = {wn[i][2], wn[i][3]};
-      a01 = a01 + s2 * w01;
-      a23 = a23 + s2 * w23;
-    }
-    float acc[4] = {a01[0], a01[1], a23[0], a23[1]};
-#pragma unroll
-    for (int c = 0; c < 4; ++c) acc[c] = wsum16(acc[c]);
-    if (L.rg == 0)
-#pragma unroll
-      for (int c = 0; c < 4; ++c)
-        if (m + c < M) Pout[slice * M + m + c] = acc[c];
+constexpr int kHistWords = 4 * 16 * kHS;  // one block: 4 waves x 16 columns
+
+// The consensus search of this lane's 4 columns over the wave's normalised
+// validator rows (wn, s: rows rg + 16 i, padding rows hold wn = 0, s = 0).
+// `ut`: the slice's stakes in units of 2^-24 when they are exact (k_rowsum /
+// the fused reducer), else -1. `hb`: this wave's 16 x kHS histogram words.
+// Returns k* per column (C_raw = k* 2^-iters), identical in the 16 lanes of a
+// column quad.
+// Reductions over the LPC lanes that share a column quad (LPC = 16: one DPP
+// row; LPC = 32: two adjacent DPP rows, joined by a lane swap xor 16). Every
+// step pairs lanes that pair back and a + b == b + a bitwise, so all lanes
+// of the group end with identical bits.
+template <int LPC>
+__device__ __forceinline__ float red_sum(float x) {
+  x = wsum16(x);
+  if constexpr (LPC == 32) x = x + __shfl_xor(x, 16, 64);
+  return x;
+}
+template <int LPC>
+__device__ __forceinline__ int red_isum(int x) {
+  x = iwsum16(x);
+  if constexpr (LPC == 32) x = x + __shfl_xor(x, 16, 64);
+  return x;
+}
+template <int LPC>
+__device__ __forceinline__ int red_imax(int x) {
+  x = iwmax16(x);
+  if constexpr (LPC == 32) x = max(x, __shfl_xor(x, 16, 64));
+  return x;
+}
+template <int LPC>
+__device__ __forceinline__ int red_imin(int x) {
+  x = iwmin16(x);
+  if constexpr (LPC == 32) x = min(x, __shfl_xor(x, 16, 64));
+  return x;
+}
+// exclusive prefix sum over the LPC lanes of a group (lane index rg in it)
+template <int LPC>
+__device__ __forceinline__ int red_iscan_excl(int x, int rg) {
+  int e = iscan16_excl(x);
+  if constexpr (LPC == 32) {
+    const int lower = __shfl_xor(iwsum16(x), 16, 64);  // the other row's total
+    e += rg >= 16 ? lower : 0;
   }
-  const float kappa = prm[n].kappa;
-  const int iters = prm[n].bisect_iters;
+  return e;
+}
+
+// LPC lanes per column quad: lane (cq, rg) holds rows rg + LPC i of columns
+// 4 cq .. 4 cq + 3 of the wave's 256 / LPC columns.
+template <int R, int LPC>
+__device__ __forceinline__ void consensus_search(const float (&wn)[R][4], const float (&s)[R],
+                                                 float kappa, int iters, int ut, unsigned* hb,
+                                                 int lane, int cq, int rg, int (&hi_k)[4]) {
+  constexpr int NCOL = 256 / LPC;  // columns per wave
+  constexpr int BPL = 64 / LPC;    // histogram bins per lane in the scan
   bool odd_stake = false;
 #pragma unroll
   for (int i = 0; i < R; ++i) odd_stake |= !(s[i] >= 0.0f) || s[i] == INFINITY;
@@ -761,7 +812,7 @@ __global__ __launch_bounds__(256, 3) void k_consensus_w(const float* __restrict_
   const bool bracket = !__any(odd_stake) && kappa >= 0.0f;
   const int top = 1 << iters;
   const float scale = (float)top, inv_scale = 1.0f / scale;
-  int lo_k[4], hi_k[4];
+  int lo_k[4];
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
     lo_k[c] = 0;
@@ -793,18 +844,16 @@ __global__ __launch_bounds__(256, 3) void k_consensus_w(const float* __restrict_
       }
     }
     // F(k) with every mask set, in exactly the order every F below uses
-    stot = wsum16(stot);
-    float vmax[4], vmin[4];
-    bool nanc[4];
+    stot = red_sum<LPC>(stot);
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-      imax[c] = iwmax16(imax[c]);
-      imin[c] = iwmin16(imin[c]);
-      nanc[c] = imax[c] > 0x7f800000;
-      vmax[c] = __int_as_float(imax[c]);
-      vmin[c] = imin[c] > 0 ? __int_as_float(imin[c]) : 0.0f;
-      const int gmax = vmax[c] > 0.0f ? (int)fminf(ceilf(vmax[c] * scale), scale) : 0;
-      const int gmin = vmin[c] > 0.0f ? (int)fminf(ceilf(vmin[c] * scale), scale + 1.0f) : 0;
+      imax[c] = red_imax<LPC>(imax[c]);
+      imin[c] = red_imin<LPC>(imin[c]);
+      const bool nanc = imax[c] > 0x7f800000;
+      const float vmx = __int_as_float(imax[c]);
+      const float vmn = imin[c] > 0 ? __int_as_float(imin[c]) : 0.0f;
+      const int gmax = vmx > 0.0f ? (int)fminf(ceilf(vmx * scale), scale) : 0;
+      const int gmin = vmn > 0.0f ? (int)fminf(ceilf(vmn * scale), scale + 1.0f) : 0;
       int lo_c = gmin >= 2 ? gmin - 1 : 0;
       int hi_c = gmax < 1 ? 1 : gmax;
       if (lo_c > 0 && !(stot > kappa)) {
@@ -816,8 +865,8 @@ __global__ __launch_bounds__(256, 3) void k_consensus_w(const float* __restrict_
         hi_c = top;
       }
       if (hi_c <= lo_c) hi_c = lo_c + 1;
-      lo_k[c] = nanc[c] ? 0 : lo_c;
-      hi_k[c] = nanc[c] ? top : hi_c;
+      lo_k[c] = nanc ? 0 : lo_c;
+      hi_k[c] = nanc ? top : hi_c;
     }
   }
   // Exact-stake finish (HIST): when every normalised stake is a multiple of
@@ -833,15 +882,11 @@ __global__ __launch_bounds__(256, 3) void k_consensus_w(const float* __restrict_
   int lim = 1;
   bool hist = false;
   int thr = 0;
-  if constexpr (HIST) {
-    // slice-uniform: k_rowsum checked the stakes (sx = exact units or -1)
-    const int ut = sx[slice];
-    hist = bracket && ut >= 0;
-    if (hist) {
-      lim = kHB - 1;
-      const double kd = floor((double)kappa * 16777216.0);
-      thr = ut - (kd > 33554432.0 ? 33554432 : (int)kd);
-    }
+  hist = bracket && ut >= 0;  // slice-uniform
+  if (hist) {
+    lim = kHB - 1;
+    const double kd = floor((double)kappa * 16777216.0);
+    thr = ut - (kd > 33554432.0 ? 33554432 : (int)kd);
   }
   for (;;) {
     bool active = false;
@@ -864,18 +909,17 @@ __global__ __launch_bounds__(256, 3) void k_consensus_w(const float* __restrict_
     }
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-      part[c] = wsum16(part[c]);
+      part[c] = red_sum<LPC>(part[c]);
       const bool act = hi_k[c] - lo_k[c] > lim, up = part[c] > kappa;
       lo_k[c] = (act && up) ? mid[c] : lo_k[c];
       hi_k[c] = (act && !up) ? mid[c] : hi_k[c];
     }
   }
-  if constexpr (HIST) {
+  {
     if (hist) {
-      __shared__ __attribute__((aligned(16))) unsigned hb[4 * 16 * kHS];
-      unsigned* wb = hb + L.wave * 16 * kHS;  // this wave's 16 columns
+      unsigned* wb = hb;  // this wave's NCOL columns
       uint4* wb4 = reinterpret_cast<uint4*>(wb);
-      for (int j = L.lane; j < 16 * kHS / 4; j += 64) wb4[j] = make_uint4(0u, 0u, 0u, 0u);
+      for (int j = lane; j < NCOL * kHS / 4; j += 64) wb4[j] = make_uint4(0u, 0u, 0u, 0u);
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -884,7 +928,7 @@ __global__ __launch_bounds__(256, 3) void k_consensus_w(const float* __restrict_
       for (int i = 0; i < R; ++i) su[i] = (unsigned)(s[i] * 16777216.0f);
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
-        unsigned* cb = wb + (L.cq * 4 + c) * kHS;
+        unsigned* cb = wb + (cq * 4 + c) * kHS;
         const float nlo = -(float)lo_k[c];
         const unsigned w = (unsigned)(hi_k[c] - lo_k[c]);
 #pragma unroll
@@ -904,23 +948,58 @@ __global__ __launch_bounds__(256, 3) void k_consensus_w(const float* __restrict_
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
-        const uint4 h = *reinterpret_cast<const uint4*>(wb + (L.cq * 4 + c) * kHS + 4 * L.rg);
-        int p[4];
-        p[0] = (int)h.x;
-        p[1] = p[0] + (int)h.y;
-        p[2] = p[1] + (int)h.z;
-        p[3] = p[2] + (int)h.w;
+        int p[BPL];
+        const unsigned* hc = wb + (cq * 4 + c) * kHS + BPL * rg;
+        if constexpr (BPL == 4) {
+          const uint4 h = *reinterpret_cast<const uint4*>(hc);
+          p[0] = (int)h.x;
+          p[1] = p[0] + (int)h.y;
+          p[2] = p[1] + (int)h.z;
+          p[3] = p[2] + (int)h.w;
+        } else {
+          const uint2 h = *reinterpret_cast<const uint2*>(hc);
+          p[0] = (int)h.x;
+          p[1] = p[0] + (int)h.y;
+        }
         // P(b) is non-decreasing, so {b : P(b) < thr} is a prefix [0, B);
         // bins b >= w hold P = total >= thr (κ >= 0), so B <= w and the
         // count over [1, w-1] is max(B - 1, 0) without per-bin range tests
-        const int t = thr - iscan16_excl(p[3]);
+        const int t = thr - red_iscan_excl<LPC>(p[BPL - 1], rg);
         int cnt = 0;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) cnt += p[j] < t ? 1 : 0;
-        hi_k[c] = lo_k[c] + max(iwsum16(cnt), 1);
+        for (int j = 0; j < BPL; ++j) cnt += p[j] < t ? 1 : 0;
+        hi_k[c] = lo_k[c] + max(red_isum<LPC>(cnt), 1);
       }
     }
   }
+}
+
+template <int R, bool VEC>
+__global__ __launch_bounds__(256, 3) void k_consensus_w(const float* __restrict__ W,
+                                                     const float* __restrict__ rsd,
+                                                     const float* __restrict__ sn,
+                                                     const int* __restrict__ sx,
+                                                     const yuma_params_t* __restrict__ prm, int N,
+                                                     int V, int M, long long slice0, int tiles,
+                                                     double* __restrict__ craw,
+                                                     float* __restrict__ Pout) {
+  __shared__ __attribute__((aligned(16))) unsigned hb[kHistWords];
+  const WLay L = wlay();
+  const long long slice = slice0 + blockIdx.x / tiles;
+  const int tile = blockIdx.x % tiles;
+  const int n = (int)(slice % N);
+  const int m = tile * kTileM + L.wave * 16 + L.cq * 4;
+  if (tile * kTileM + L.wave * 16 >= M) return;  // whole wave past the last miner
+  float wn[R][4], s[R];
+  load_norm_w<R, VEC, false>(W + slice * (long long)V * M, rsd + slice * V, sn + slice * V, V, M,
+                             m, L.rg, wn, s);
+  if (Pout != nullptr) prerank_store<R>(wn, s, L, m, M, Pout + slice * M);
+  int hi_k[4];
+  const yuma_params_t& p = prm[n];
+  const bool hist_ok = !(p.flags & YUMA_FLAG_NO_HIST);
+  consensus_search<R, 16>(wn, s, p.kappa, p.bisect_iters, hist_ok ? sx[slice] : -1,
+                          hb + L.wave * 16 * kHS, L.lane, L.cq, L.rg, hi_k);
+  const int top = 1 << p.bisect_iters;
   if (L.rg == 0)
 #pragma unroll
     for (int c = 0; c < 4; ++c)
@@ -1406,420 +1485,552 @@ __global__ __launch_bounds__(NT) void k_rank(
 }
 
 // ---------------------------------------------------------------------------
-// Phase 1 fused (rowsum + consensus + quantise + rank in ONE read of W).
-// Work items (slice, 64-miner tile) are dequeued in slice-major order by a
-// persistent grid; each block keeps its W tile in registers across two
-// intra-slice hand-offs:
-//   (1) row-sum partials of every tile -> the last arriving block reduces
-//       them to rs[V] (+ S/sum S) and raises flag_rs;
-//   (2) per-tile sums of C_raw -> the last arriver forms sum C, raises flag_c.
-// Protocol (cdna_hip_programming.md Guideline 16): plain stores, every wave
-// s_waitcnt vmcnt(0), barrier, one lane agent-release + asm wait + relaxed
-// atomic; consumers poll one word relaxed with s_sleep, one agent acquire,
-// wait + barrier, then vector loads. Deadlock-free: a block only waits on its
-// own slice, every item of an earlier slice was dequeued before it, and the
-// host only uses this kernel when tiles <= resident blocks / 2. Spins are
-// bounded (timeout word in the sync block).
+// Fused phase 1 (k_fused1): row sums, stake normalisation, consensus,
+// quantisation and rank (yumas.py:186-217; YumaRust :72-106, C in fp64) of
+// every slice in ONE read of W, for run outputs with 32 <= V <= 256.
+//
+// Geometry: one persistent block of 4 waves per CU (one wave per SIMD: the
+// whole 512-register file per lane). The T = ceil(M / 32) tiles of a slice
+// belong to a GROUP of T blocks: block j of a group owns miners
+// 32 j .. 32 j + 31 of every slice of the group, and group g takes the slices
+// g, g + G, g + 2G, ... of the chunk. Wave w owns 8 of the tile's miners;
+// lane (cq = lane / 32, rg = lane % 32) owns 4 of them in validator rows
+// rg + 32 r (r < 8), so every column reduction (consensus, rank) is a
+// 32-lane DPP/swizzle tree inside one wave, with no barrier.
+//
+// Cross-block data moves as tagged 8-byte granules {value, tag}
+// (cdna_hip_programming.md Guideline 16, R2: the data is the flag): the
+// producer writes each with ONE agent-scope (write-through) store and never
+// waits; the consumer sweeps them with agent-scope loads until every tag
+// matches. A hop costs two iterations: data published during iteration k is
+// swept at the end of iteration k + 1 (issued after everything else, so the
+// snapshot is a whole iteration old; its wait at the start of iteration k + 2
+// leaves the younger tile loads in flight) and used in iteration k + 2.
+// Stages of the i-th slice of a group:
+//   iteration i-1  L  load the tile (8 float4 per lane, registers)
+//   iteration i    P  row partials over the tile's 32 miners -> rowpart[i];
+//                     the raw tile moves to the LDS ring (4 x 32 KB)
+//   iteration i+2  D  block j sums its rows (j rpb .. j rpb + rpb - 1) over
+//                     the T partials in tile order, + 1e-6   -> rowsum[i]
+//   iteration i+4  C  S / sum S, the tile back from LDS, normalise,
+//                     consensus; tile sum of C_raw            -> cpart[i]
+//   iteration i+6  K  sum C over tiles, quantise own columns, clip, rank
+// The granules sit in rings of kF1Ring slots per group (tag = i + 1), zeroed
+// by a memset node before every launch. Every sweep is bounded: a timeout
+// raises ctl[1] (yuma_status reports it) instead of hanging the GPU.
+//
+// Summation orders are fixed (bitwise reproducible) and shared with the
+// multi-pass path: a row's tile partial is the balanced tree over the tile's
+// 8 column quads of the sequential quad sums (k_rowsum computes the same),
+// a row sum adds the tile partials in tile order, then 1e-6; sum S is
+// k_rowsum's lane-strided sum and butterfly.
 // ---------------------------------------------------------------------------
-struct P1Args {
+constexpr int kF1Ring = 8;
+constexpr int kF1Tile = 32;              // miners per block tile
+constexpr int kF1R = 8;                  // validator rows per lane
+constexpr int kF1Slots = 4;              // LDS ring of raw tiles (P -> C)
+constexpr int kF1MaxBlocks = 256;        // persistent blocks (one per CU)
+constexpr unsigned kF1Spin = 1u << 22;   // polls (each after s_sleep) before giving up
+// LDS words: ring[4][4 waves][8 r][64 lanes][4] | hist | red[4][256] | dred[512]
+//            | rsd[256] | sn[256] | sraw[256] | cp[2][256] | misc[64]
+constexpr int kF1Ring0 = 0;
+constexpr int kF1Hist = kF1Slots * 4 * kF1R * 64 * 4;
+constexpr int kF1Red = kF1Hist + 4 * 8 * kHS;
+constexpr int kF1Dred = kF1Red + 4 * 256;
+constexpr int kF1Rsd = kF1Dred + 512;
+constexpr int kF1Sn = kF1Rsd + 256;
+constexpr int kF1Sraw = kF1Sn + 256;
+constexpr int kF1Cp = kF1Sraw + 256;
+constexpr int kF1Misc = kF1Cp + 512;
+constexpr int kF1Lds = kF1Misc + 64;
+static_assert(kF1Lds * 4 <= 160 * 1024, "k_fused1 LDS");
+
+struct F1Args {
   const float* W;
   const float* S;
   const yuma_params_t* prm;
-  int N, V, M, tiles, variant;
-  long long slice0, nslices;
-  float* rsd;
-  float* sn;
-  double* craw;
-  float* C;
-  int* qlev;
-  float* R;
-  float* rpart;
-  float* P;
-  float* Wn_out;
-  float* Wc_out;
-  float* tvc;
-  float* tvn;
-  unsigned* sync;    // [nslices][4] cnt_rs, flag_rs, cnt_c, flag_c; then head, timeout
-  float* rowpart;    // [nslices][tiles][V]
-  float* cpart_f;    // [nslices][tiles]
-  double* cpart_d;   // [nslices][tiles]
-  float* sumc_f;     // [nslices]
-  double* sumc_d;    // [nslices]
+  int N, V, M, T, G, rpb, nch, rust;
+  int s0, ns;
+  float* rsd;      // [slice][V] (absolute slice index)
+  float* sn;       // [slice][V]
+  int* sx;         // [slice]
+  float* C;        // [slice][M]
+  int* qlev;       // [slice][M]
+  float* R;        // [slice][M]
+  float* rpart;    // [slice][T]
+  float* sumc_f;   // [ns] (chunk-local slice index)
+  double* sumc_d;  // [ns]
+  unsigned long long* g_rowpart;  // [G][ring][T][V]
+  unsigned long long* g_rowsum;   // [G][ring][V]
+  unsigned long long* g_cpart;    // [G][ring][T][2]
+  unsigned* ctl;                  // [0] ticket, [1] timeout, [2..3] poll counters
 };
 
-constexpr unsigned kSpinLimit = 1u << 22;
+typedef __attribute__((address_space(1))) unsigned long long g_u64;
+typedef __attribute__((address_space(1))) unsigned g_u32;
 
-__device__ __forceinline__ unsigned ld_relaxed(const unsigned* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+__device__ __forceinline__ void put_granule(unsigned long long* p, unsigned tag, unsigned val) {
+  __hip_atomic_store((g_u64*)p, ((unsigned long long)tag << 32) | val, __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
 }
-// Hand-off form (MI355X_MICROARCH.md visibility table, row 1): every
-// handed-off word is stored with an agent-scope relaxed atomic store (sc1,
-// write-through) and read with an agent-scope relaxed atomic load (sc1,
-// bypasses L1); every storing wave drains (vmcnt(0)) before the workgroup
-// barrier; one lane then signals with an agent atomic. No release/acquire
-// fences (each one writes back / invalidates a whole cache level).
-template <typename Tv>
-__device__ __forceinline__ void st_sc1(Tv* p, Tv v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+__device__ __forceinline__ unsigned long long get_granule(const unsigned long long* p) {
+  return __hip_atomic_load((const g_u64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-template <typename Tv>
-__device__ __forceinline__ Tv ld_sc1(const Tv* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// every thread calls; returns the counter value before this block's add
-__device__ __forceinline__ unsigned arrive(unsigned* cnt, unsigned* sh) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0)
-    *sh = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __syncthreads();
-  return *sh;
-}
-__device__ __forceinline__ void acquire_block() {
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler ordering only
-  __syncthreads();
-}
-__device__ __forceinline__ void raise_flag(unsigned* flag) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) __hip_atomic_store(flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void wait_flag(const unsigned* flag, unsigned* timeout) {
-  if (threadIdx.x == 0) {
+// The value of a swept granule; polls again (bounded) while its tag is not
+// `tag` (the rare path: its loads wait for everything in flight).
+__device__ __forceinline__ unsigned settle(const unsigned long long* p, unsigned long long x,
+                                          unsigned tag, unsigned* ctl, unsigned& polls) {
+  if ((unsigned)(x >> 32) != tag) {
     unsigned spins = 0;
-    while (ld_relaxed(flag) == 0u) {
+    do {
       __builtin_amdgcn_s_sleep(2);
-      if (++spins > kSpinLimit) {
-        __hip_atomic_store(timeout, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      x = get_granule(p);
+      if (++spins > kF1Spin) {
+        __hip_atomic_store((g_u32*)(ctl + 1), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
+      }
+    } while ((unsigned)(x >> 32) != tag);
+    polls += spins;
+  }
+  return (unsigned)x;
+}
+
+// Packed row division wn = RN(w / d) (div_fast_nz on pairs, lane-wide guard;
+// see load_norm_w); returns true when some operand is outside the guard.
+template <int R>
+__device__ __forceinline__ bool norm_packed(float (&wn)[R][4], const float (&d)[R]) {
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  float amax = 0.0f, dmin = INFINITY;
+  unsigned ymin = 0xFFFFFFFFu;
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    const float r = 1.0f / d[i];
+    amax = fmaxf(amax, fabsf(d[i]));
+    dmin = fminf(dmin, fabsf(d[i]));
+    const f2 r2 = {r, r}, nd2 = {-d[i], -d[i]};
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const f2 a2 = {wn[i][2 * h], wn[i][2 * h + 1]};
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        amax = fmaxf(amax, fabsf(a2[c]));
+        const unsigned y = (__float_as_uint(a2[c]) << 1) - 1u;
+        ymin = y < ymin ? y : ymin;
+      }
+      const f2 q = a2 * r2;
+      const f2 e = __builtin_elementwise_fma(nd2, q, a2);
+      const f2 q1 = __builtin_elementwise_fma(e, r2, q);
+      wn[i][2 * h] = q1[0];
+      wn[i][2 * h + 1] = q1[1];
+    }
+  }
+  return !(dmin >= 0x1p-60f && amax <= 0x1p60f &&
+           (ymin == 0xFFFFFFFFu || ymin + 1u >= (__float_as_uint(0x1p-60f) << 1)));
+}
+
+struct F1Ctx {
+  int V, M, T, G, rpb, nch, g, j, m, tid, lane, wave, cq, rg, nq, VM;
+  int dk0, dk1;  // this thread's D granule columns (row * V-offset resolved)
+  bool rust, small_idx, edge;
+  unsigned* lds;
+};
+// the swept granules of one iteration (issued at the end of the previous one)
+struct F1Sweep {
+  unsigned long long d0, d1, c, k0, k1;
+  float sraw;
+};
+
+__device__ __forceinline__ int f1_slice(const F1Args& A, const F1Ctx& c, int i) {
+  const int k = i < c.nq ? (i < 0 ? 0 : i) : c.nq - 1;
+  return A.s0 + c.g + c.G * k;
+}
+__device__ __forceinline__ int f1_ring(const F1Ctx& c, int i) {
+  return c.g * kF1Ring + ((i < 0 ? 0 : i) & (kF1Ring - 1));
+}
+__device__ __forceinline__ unsigned long long* f1_pD(const F1Args& A, const F1Ctx& c, int i, int dk) {
+  return A.g_rowpart + (long long)f1_ring(c, i) * c.T * c.V + dk;
+}
+__device__ __forceinline__ unsigned long long* f1_pC(const F1Args& A, const F1Ctx& c, int i) {
+  return A.g_rowsum + f1_ring(c, i) * c.V + min(c.tid, c.V - 1);
+}
+__device__ __forceinline__ unsigned long long* f1_pK(const F1Args& A, const F1Ctx& c, int i) {
+  return A.g_cpart + (f1_ring(c, i) * c.T + min(c.tid, c.T - 1)) * 2;
+}
+
+// Sweep loads of iteration i (D: rowpart of slice i-2, C: rowsum of slice
+// i-4 and its raw stakes, K: cpart of slice i-6), issued at the end of
+// iteration i-1.
+__device__ __forceinline__ void f1_sweep(const F1Args& A, const F1Ctx& c, int i, F1Sweep& w) {
+  const int nD = c.rpb * c.T;
+  w.d0 = w.d1 = w.c = w.k0 = w.k1 = 0;
+  w.sraw = 0.0f;
+  if (c.tid < nD) w.d0 = get_granule(f1_pD(A, c, i - 2, c.dk0));
+  if (c.tid + 256 < nD) w.d1 = get_granule(f1_pD(A, c, i - 2, c.dk1));
+  if (c.tid < c.V) {
+    w.c = get_granule(f1_pC(A, c, i - 4));
+    w.sraw = A.S[(long long)f1_slice(A, c, i - 4) * c.V + c.tid];
+  }
+  if (c.tid < c.T) {
+    w.k0 = get_granule(f1_pK(A, c, i - 6));
+    if (c.rust) w.k1 = get_granule(f1_pK(A, c, i - 6) + 1);
+  }
+}
+
+// branch-free tile loads (rows >= V and columns >= M read in-range
+// addresses and are zeroed later)
+__device__ __forceinline__ void f1_load(const F1Args& A, const F1Ctx& c, float (&t)[kF1R][4], int i) {
+  const float* Ws = A.W + (long long)f1_slice(A, c, i) * c.VM;
+  const int mm = c.m < c.M ? c.m : c.M - 4;
+#pragma unroll
+  for (int r = 0; r < kF1R; ++r) {
+    const int rr = min(c.rg + 32 * r, c.V - 1);
+    const float* p = c.small_idx ? Ws + ((unsigned)rr * (unsigned)c.M + (unsigned)mm)
+                                 : Ws + ((long long)rr * c.M + mm);
+    const fvec4 x = *reinterpret_cast<const fvec4*>(p);
+    t[r][0] = x.x;
+    t[r][1] = x.y;
+    t[r][2] = x.z;
+    t[r][3] = x.w;
+  }
+}
+__device__ __forceinline__ void f1_mask(const F1Ctx& c, float (&t)[kF1R][4]) {
+  if (!c.edge) return;  // block-uniform: only edge tiles hold padding
+#pragma unroll
+  for (int r = 0; r < kF1R; ++r)
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (c.rg + 32 * r >= c.V || c.m + k >= c.M) t[r][k] = 0.0f;
+}
+// this wave's part of LDS ring slot `slot` (lane-contiguous float4 per row)
+__device__ __forceinline__ fvec4* f1_slot(const F1Ctx& c, int slot) {
+  return reinterpret_cast<fvec4*>(c.lds + kF1Ring0) + ((slot * 4 + c.wave) * kF1R) * 64 + c.lane;
+}
+
+// Iteration i; U = i mod 2 selects the register sets: tl[U ^ 1] receives
+// slice i+1, tl[U] holds slice i (P); tn[U] holds the normalised slice i-6
+// (K) and then receives slice i-4 (C).
+template <int U>
+__device__ __forceinline__ void f1_iter(const F1Args& A, const F1Ctx& c, int i, F1Sweep& w,
+                                        float (&tl)[2][kF1R][4], float (&tn)[2][kF1R][4],
+                                        float (&skeep)[2][kF1R], int (&hk)[2][4], unsigned& polls) {
+  constexpr int R = kF1R;
+  float* red = reinterpret_cast<float*>(c.lds + kF1Red);
+  float* dred = reinterpret_cast<float*>(c.lds + kF1Dred);
+  float* rsd_l = reinterpret_cast<float*>(c.lds + kF1Rsd);
+  float* sn_l = reinterpret_cast<float*>(c.lds + kF1Sn);
+  float* sraw_l = reinterpret_cast<float*>(c.lds + kF1Sraw);
+  unsigned* cp_l = c.lds + kF1Cp;
+  unsigned* misc = c.lds + kF1Misc;
+  const int tid = c.tid, V = c.V, T = c.T, nq = c.nq;
+  const bool doP = i < nq, doD = i >= 2 && i - 2 < nq, doC = i >= 4 && i - 4 < nq,
+             doK = i >= 6 && i - 6 < nq;
+  const int iD = i - 2, iC = i - 4, iK = i - 6;
+
+  // 1. the next tile
+  f1_load(A, c, tl[U ^ 1], i + 1);
+  // 2. settle this iteration's sweeps (older than the tile loads)
+  const int nD = c.rpb * T;
+  if (doD && tid < nD)
+    dred[tid] = __uint_as_float(settle(f1_pD(A, c, iD, c.dk0), w.d0, (unsigned)(iD + 1), A.ctl, polls));
+  if (doD && tid + 256 < nD)
+    dred[tid + 256] = __uint_as_float(settle(f1_pD(A, c, iD, c.dk1), w.d1, (unsigned)(iD + 1), A.ctl, polls));
+  if (doC && tid < V) {
+    rsd_l[tid] = __uint_as_float(settle(f1_pC(A, c, iC), w.c, (unsigned)(iC + 1), A.ctl, polls));
+    sraw_l[tid] = w.sraw;
+  }
+  if (doK && tid < T) {
+    cp_l[tid] = settle(f1_pK(A, c, iK), w.k0, (unsigned)(iK + 1), A.ctl, polls);
+    if (c.rust) cp_l[256 + tid] = settle(f1_pK(A, c, iK) + 1, w.k1, (unsigned)(iK + 1), A.ctl, polls);
+  }
+  // 3. P: row partials of tile i over its 32 miners
+  if (doP) {
+    f1_mask(c, tl[U]);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const float a = ((tl[U][r][0] + tl[U][r][1]) + tl[U][r][2]) + tl[U][r][3];
+      const float b = a + __shfl_xor(a, 32, 64);  // the wave's two quads
+      if (c.cq == 0) red[c.wave * 256 + c.rg + 32 * r] = b;
+    }
+  }
+  __syncthreads();  // B1
+
+  // 4. publish P; D on wave 0; sum C (wave 2); S / sum S (wave 3)
+  if (doP && tid < V) {
+    const float part = (red[tid] + red[256 + tid]) + (red[512 + tid] + red[768 + tid]);
+    put_granule(A.g_rowpart + ((long long)f1_ring(c, i) * T + c.j) * V + tid, (unsigned)(i + 1),
+                __float_as_uint(part));
+  }
+  if (doD && c.wave == 0) {
+    // row sum = the 256-miner chunk partials (balanced tree over 8 tiles) in
+    // chunk order, + 1e-6 (k_rowsum's order). Lane L < rpb nch: chunk
+    // L % nch of own row L / nch.
+    const int nch = c.nch;
+    float cpv = 0.0f;
+    if (c.lane < c.rpb * nch) {
+      const int dr = c.lane / nch, ch = c.lane - dr * nch;
+      float p8[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int t = ch * 8 + k;
+        p8[k] = t < T ? dred[dr * T + t] : 0.0f;
+      }
+      cpv = ((p8[0] + p8[1]) + (p8[2] + p8[3])) + ((p8[4] + p8[5]) + (p8[6] + p8[7]));
+    }
+    float mine = 0.0f;
+    for (int dr = 0; dr < c.rpb; ++dr) {
+      float acc = 0.0f;
+      for (int ch = 0; ch < nch; ++ch) acc = acc + __shfl(cpv, dr * nch + ch, 64);
+      mine = c.lane == dr ? acc : mine;
+    }
+    const int v = c.j * c.rpb + c.lane;
+    if (c.lane < c.rpb && v < V) {
+      const float rs = mine + 1e-6f;
+      put_granule(A.g_rowsum + f1_ring(c, iD) * V + v, (unsigned)(iD + 1), __float_as_uint(rs));
+      A.rsd[(long long)f1_slice(A, c, iD) * V + v] = rs;
+    }
+  }
+  if (doK && c.wave == 2) {
+    // sum C over tiles: lane-strided, then the wave butterfly (fixed order)
+    if (c.rust) {
+      double a = 0.0;
+      for (int t = c.lane; t < T; t += 64)
+        a = a + __hiloint2double((int)cp_l[256 + t], (int)cp_l[t]);
+      a = wave_sum_d(a);
+      if (c.lane == 0) {
+        misc[2] = (unsigned)__double2loint(a);
+        misc[3] = (unsigned)__double2hiint(a);
+      }
+    } else {
+      float a = 0.0f;
+      for (int t = c.lane; t < T; t += 64) a = a + __uint_as_float(cp_l[t]);
+      a = wave_sum(a);
+      if (c.lane == 0) misc[2] = __float_as_uint(a);
+    }
+  }
+  if (doC && c.wave == 3) {
+    // S / S.sum() (yumas.py:189) in k_rowsum's order, and the exact-stake
+    // units (or -1) of the consensus histogram finish
+    const int slC = f1_slice(A, c, iC);
+    float acc = 0.0f;
+    for (int v = c.lane; v < V; v += 64) acc = acc + sraw_l[v];
+    acc = wave_sum(acc);
+    int units = 0;
+    bool exact = true;
+    for (int v = c.lane; v < V; v += 64) {
+      const float q = sraw_l[v] / acc;
+      sn_l[v] = q;
+      if (c.j == 0) A.sn[(long long)slC * V + v] = q;
+      const float f = q * 16777216.0f;
+      exact &= f >= 0.0f && f <= 16777216.0f && __builtin_amdgcn_fractf(f) == 0.0f;
+      units += exact ? (int)f : 0;
+    }
+    for (int o = 1; o < 64; o <<= 1) units += __shfl_xor(units, o, 64);
+    exact = __all(exact) && units <= (1 << 24);
+    if (c.lane == 0) {
+      misc[4] = (unsigned)(exact ? units : -1);
+      if (c.j == 0) A.sx[slC] = exact ? units : -1;
+    }
+  }
+  __syncthreads();  // B2
+
+  // 5. K: quantise slice i-6's columns with sum C, clip, rank (tn[U])
+  if (doK) {
+    const int slK = f1_slice(A, c, iK);
+    const yuma_params_t& p = A.prm[slK % A.N];
+    float Cq[4];
+    int lev[4];
+    if (c.rust) {
+      const double sumd = __hiloint2double((int)misc[3], (int)misc[2]);
+      const double it = 1.0 / (double)(1 << p.bisect_iters);  // exact (power of two)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) lev[k] = (int)((double)hk[U][k] * it / sumd * 65535.0);
+    } else {
+      const RowDiv sd = row_div(__uint_as_float(misc[2]));
+      const float it = 1.0f / (float)(1 << p.bisect_iters);  // exact (power of two)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) lev[k] = (int)(div_rn((float)hk[U][k] * it, sd) * 65535.0f);
+    }
+    const RowDiv q65535 = row_div(65535.0f);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) Cq[k] = c.m + k < c.M ? div_rn((float)lev[k], q65535) : 0.0f;
+    float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) acc[k] = acc[k] + skeep[U][r] * vmin(tn[U][r][k], Cq[k]);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) acc[k] = red_sum<32>(acc[k]);
+    if (c.rg == 0 && c.m < c.M) {
+      const long long o = (long long)slK * c.M + c.m;
+      *reinterpret_cast<fvec4*>(A.R + o) = fvec4{acc[0], acc[1], acc[2], acc[3]};
+      *reinterpret_cast<fvec4*>(A.C + o) = fvec4{Cq[0], Cq[1], Cq[2], Cq[3]};
+      *reinterpret_cast<int4*>(A.qlev + o) = make_int4(lev[0], lev[1], lev[2], lev[3]);
+    }
+    float ws = ((acc[0] + acc[1]) + acc[2]) + acc[3];
+    ws = ws + __shfl_xor(ws, 32, 64);
+    if (c.lane == 0) misc[32 + c.wave] = __float_as_uint(ws);
+  }
+  // 6. C: slice i-4 back from the ring, normalise, consensus (into tn[U])
+  if (doC) {
+    const int slC = f1_slice(A, c, iC);
+    const yuma_params_t& p = A.prm[slC % A.N];
+    const fvec4* src = f1_slot(c, iC & (kF1Slots - 1));
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const fvec4 x = src[r * 64];
+      tn[U][r][0] = x.x;
+      tn[U][r][1] = x.y;
+      tn[U][r][2] = x.z;
+      tn[U][r][3] = x.w;
+    }
+    float d[R], s[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int row = c.rg + 32 * r, rr = min(row, V - 1);
+      d[r] = rsd_l[rr];
+      s[r] = row < V ? sn_l[rr] : 0.0f;
+    }
+    if (__any(norm_packed<R>(tn[U], d))) {  // rare: IEEE division from W
+      f1_load(A, c, tn[U], iC);
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) tn[U][r][k] = tn[U][r][k] / d[r];
+    }
+    f1_mask(c, tn[U]);
+    const int ut = (p.flags & YUMA_FLAG_NO_HIST) ? -1 : (int)misc[4];
+    int hi[4];
+    consensus_search<R, 32>(tn[U], s, p.kappa, p.bisect_iters, ut, c.lds + kF1Hist + c.wave * 8 * kHS,
+                            c.lane, c.cq, c.rg, hi);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) hk[U][k] = hi[k];
+#pragma unroll
+    for (int r = 0; r < R; ++r) skeep[U][r] = s[r];
+    // tile partial of C_raw (quads sequential, the two quads, waves below)
+    if (c.rust) {
+      const double it = 1.0 / (double)(1 << p.bisect_iters);
+      double a = 0.0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) a = a + (c.m + k < c.M ? (double)hi[k] * it : 0.0);
+      a = a + __shfl_xor(a, 32, 64);
+      if (c.lane == 0) {
+        misc[16 + 2 * c.wave] = (unsigned)__double2loint(a);
+        misc[17 + 2 * c.wave] = (unsigned)__double2hiint(a);
+      }
+    } else {
+      const float it = 1.0f / (float)(1 << p.bisect_iters);
+      float a = 0.0f;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) a = a + (c.m + k < c.M ? (float)hi[k] * it : 0.0f);
+      a = a + __shfl_xor(a, 32, 64);
+      if (c.lane == 0) misc[16 + c.wave] = __float_as_uint(a);
+    }
+  }
+  // 7. the raw tile i into the ring (its slot held slice i-4, read above by
+  //    this same wave: each wave owns its part of a slot)
+  if (doP) {
+    fvec4* dst = f1_slot(c, i & (kF1Slots - 1));
+#pragma unroll
+    for (int r = 0; r < R; ++r) dst[r * 64] = fvec4{tl[U][r][0], tl[U][r][1], tl[U][r][2], tl[U][r][3]};
+  }
+  __syncthreads();  // B3
+  if (doC && tid == 0) {
+    unsigned long long* pc = A.g_cpart + (f1_ring(c, iC) * T + c.j) * 2;
+    if (c.rust) {
+      double q[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) q[k] = __hiloint2double((int)misc[17 + 2 * k], (int)misc[16 + 2 * k]);
+      const double a = (q[0] + q[1]) + (q[2] + q[3]);
+      put_granule(pc, (unsigned)(iC + 1), (unsigned)__double2loint(a));
+      put_granule(pc + 1, (unsigned)(iC + 1), (unsigned)__double2hiint(a));
+    } else {
+      float q[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) q[k] = __uint_as_float(misc[16 + k]);
+      put_granule(pc, (unsigned)(iC + 1), __float_as_uint((q[0] + q[1]) + (q[2] + q[3])));
+    }
+  }
+  if (doK && tid == 64) {
+    const int slK = f1_slice(A, c, iK);
+    float q[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) q[k] = __uint_as_float(misc[32 + k]);
+    A.rpart[(long long)slK * T + c.j] = (q[0] + q[1]) + (q[2] + q[3]);
+    if (c.j == 0) {
+      const int ls = slK - A.s0;
+      if (c.rust) {
+        const double sd = __hiloint2double((int)misc[3], (int)misc[2]);
+        A.sumc_d[ls] = sd;
+        A.sumc_f[ls] = (float)sd;
+      } else {
+        A.sumc_f[ls] = __uint_as_float(misc[2]);
       }
     }
   }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler ordering only
-  __syncthreads();
+  // 8. the sweeps of iteration i+1: a whole iteration after their producers
+  f1_sweep(A, c, i + 1, w);
 }
 
-template <int NT, int R, bool VEC>
-__global__ __launch_bounds__(NT, NT == 256 ? 3 : 1) void k_phase1(P1Args A) {
-  constexpr int NW = NT / 64, G = NT / 16;
-  __shared__ float4 red[2][NW * 16];
-  __shared__ unsigned sh_u;
-  __shared__ float shf[NW];
-  __shared__ double shd[NW];
-  const Lay L = lay();
-  const int V = A.V, M = A.M, T = A.tiles;
-  const long long total = A.nslices * T;
-  unsigned* head = A.sync + 4 * A.nslices;
-  unsigned* timeout = head + 1;
-  const bool rust = A.variant == YUMA_VARIANT_RUST;
+__global__ __launch_bounds__(256, 1) void k_fused1(F1Args A) {
+  __shared__ __attribute__((aligned(16))) unsigned lds[kF1Lds];
+  F1Ctx c;
+  c.tid = threadIdx.x;
+  c.lane = c.tid & 63;
+  c.wave = c.tid >> 6;
+  c.cq = c.lane >> 5;
+  c.rg = c.lane & 31;
+  c.lds = lds;
+  if (c.tid == 0)
+    lds[kF1Misc] = __hip_atomic_fetch_add((g_u32*)A.ctl, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  const int ticket = (int)lds[kF1Misc];
+  c.V = A.V;
+  c.M = A.M;
+  c.T = A.T;
+  c.G = A.G;
+  c.rpb = A.rpb;
+  c.nch = A.nch;
+  c.g = ticket / A.T;
+  c.j = ticket - c.g * A.T;
+  if (c.g >= A.G) return;  // the whole block (uniform)
+  c.nq = (A.ns - c.g + A.G - 1) / A.G;
+  if (c.nq <= 0) return;
+  c.VM = A.V * A.M;
+  c.m = c.j * kF1Tile + c.wave * 8 + c.cq * 4;
+  c.rust = A.rust != 0;
+  c.small_idx = c.VM < (1 << 30);
+  c.edge = A.V < 256 || (c.j + 1) * kF1Tile > A.M;
+  // D granule columns: entry k = (own row k / T, tile k % T)
+  c.dk0 = (c.tid % A.T) * A.V + min(c.j * A.rpb + c.tid / A.T, A.V - 1);
+  c.dk1 = ((c.tid + 256) % A.T) * A.V + min(c.j * A.rpb + (c.tid + 256) / A.T, A.V - 1);
+  float tl[2][kF1R][4];
+  float tn[2][kF1R][4];
+  float skeep[2][kF1R];
+  int hk[2][4];
+  unsigned polls = 0;
+  F1Sweep w;
+  f1_load(A, c, tl[0], 0);
+  f1_sweep(A, c, 0, w);
+  for (int i0 = 0;; i0 += 2) {
+    f1_iter<0>(A, c, i0, w, tl, tn, skeep, hk, polls);
+    f1_iter<1>(A, c, i0 + 1, w, tl, tn, skeep, hk, polls);
+    if (i0 + 2 > c.nq + 5) break;
+  }
+  // diagnostics: one add per wave that polled
+  const unsigned wp = (unsigned)__reduce_add_sync(~0ull, (int)polls);
+  if (c.lane == 0 && wp != 0u) {
+    __hip_atomic_fetch_add((g_u32*)(A.ctl + 2), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add((g_u32*)(A.ctl + 3), wp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
 
-  for (;;) {
-    if (threadIdx.x == 0) sh_u = __hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-    const long long item = sh_u;
-    __syncthreads();
-    if (item >= total) break;
-    const long long ls = item / T;  // slice within the chunk
-    const int tile = (int)(item % T);
-    const long long slice = A.slice0 + ls;
-    const int n = (int)(slice % A.N);
-    const int m = tile * kTileM + L.c4 * 4;
-    unsigned* sy = A.sync + 4 * ls;
-
-    // ---- load the tile (one HBM read of W per element, all loads in flight)
-    float x[R][4];
-#pragma unroll
-    for (int i = 0; i < R; ++i) load4c<VEC>(A.W + slice * (long long)V * M, L.g + G * i, V, m, M, x[i]);
-    // ---- (1) row-sum partials of this tile
-#pragma unroll
-    for (int i = 0; i < R; ++i) {
-      float a = 0.0f;
-#pragma unroll
-      for (int c = 0; c < 4; ++c)
-        if (m + c < M) a = a + x[i][c];
-      a = sum_row16(a);
-      const int row = L.g + G * i;
-      if (L.c4 == 0 && row < V) st_sc1(&A.rowpart[(ls * T + tile) * V + row], a);
-    }
-    if (arrive(&sy[0], &sh_u) == (unsigned)(T - 1)) {
-      // last arriver: rs[v] = sum over tiles (tile order), S / sum S
-      acquire_block();
-      for (int v = threadIdx.x; v < V; v += NT) {
-        // 16 loads in flight per batch; sums stay in tile order
-        float a = 0.0f;
-        int k = 0;
-        for (; k + 16 <= T; k += 16) {
-          float t[16];
-#pragma unroll
-          for (int j = 0; j < 16; ++j) t[j] = ld_sc1(&A.rowpart[(ls * T + k + j) * V + v]);
-#pragma unroll
-          for (int j = 0; j < 16; ++j) a = a + t[j];
-        }
-        for (; k < T; ++k) a = a + ld_sc1(&A.rowpart[(ls * T + k) * V + v]);
-        st_sc1(&A.rsd[slice * V + v], a + 1e-6f);
-      }
-      float sacc = 0.0f;
-      for (int v = threadIdx.x; v < V; v += NT) sacc = sacc + A.S[slice * V + v];
-      const float stot = block_sum<NT>(sacc, shf);
-      for (int v = threadIdx.x; v < V; v += NT) st_sc1(&A.sn[slice * V + v], A.S[slice * V + v] / stot);
-      raise_flag(&sy[1]);
-    }
-    wait_flag(&sy[1], timeout);
-
-    // ---- normalise in place (rows, stakes are hand-off data: vector loads
-    // after the acquire)
-    float (&wn)[R][4] = x;
-    float s[R];
-    {
-      float dv[R];
-      bool slow = false;
-#pragma unroll
-      for (int i = 0; i < R; ++i) {
-        const int rr = min(L.g + G * i, V - 1);
-        dv[i] = ld_sc1(&A.rsd[slice * V + rr]);
-        s[i] = ld_sc1(&A.sn[slice * V + rr]);
-      }
-#pragma unroll
-      for (int i = 0; i < R; ++i) {
-        const RowDiv rdv = row_div(dv[i]);
-#pragma unroll
-        for (int c = 0; c < 4; ++c) wn[i][c] = div_fast(x[i][c], rdv, slow);
-      }
-      if (__syncthreads_or(slow)) {
-#pragma unroll
-        for (int i = 0; i < R; ++i) {
-          load4c<VEC>(A.W + slice * (long long)V * M, L.g + G * i, V, m, M, wn[i]);
-#pragma unroll
-          for (int c = 0; c < 4; ++c) wn[i][c] = wn[i][c] / dv[i];
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < R; ++i) {
-        mask4(L.g + G * i, V, m, M, wn[i]);
-        if (L.g + G * i >= V) s[i] = 0.0f;
-      }
-    }
-    if (A.P != nullptr) {
-      float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-      for (int i = 0; i < R; ++i)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) acc[c] = acc[c] + s[i] * wn[i][c];
-      col_reduce4<NW>(acc, red[1], L);
-      if (L.g == 0)
-#pragma unroll
-        for (int c = 0; c < 4; ++c)
-          if (m + c < M) A.P[slice * M + m + c] = acc[c];
-      __syncthreads();
-    }
-
-    // ---- consensus: bracketed exact search (see k_consensus)
-    const float kappa = A.prm[n].kappa;
-    const int iters = A.prm[n].bisect_iters;
-    int hi_k[4];
-    {
-      bool odd_stake = false;
-#pragma unroll
-      for (int i = 0; i < R; ++i) odd_stake |= !(s[i] >= 0.0f) || s[i] == INFINITY;
-      const bool bracket = !__syncthreads_or(odd_stake) && kappa >= 0.0f;
-      const int top = 1 << iters;
-      const float scale = (float)top, inv_scale = 1.0f / scale;
-      int lo_k[4];
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        lo_k[c] = 0;
-        hi_k[c] = top;
-      }
-      if (bracket) {
-        float vmax[4], vmin[4], stot[4];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          vmax[c] = -INFINITY;
-          vmin[c] = INFINITY;
-          stot[c] = 0.0f;
-        }
-#pragma unroll
-        for (int i = 0; i < R; ++i) {
-          if (L.g + G * i >= V) continue;
-#pragma unroll
-          for (int c = 0; c < 4; ++c) {
-            const float xv = wn[i][c];
-            vmax[c] = xv > vmax[c] ? xv : vmax[c];
-            const float xm = xv == xv ? xv : 0.0f;
-            vmin[c] = xm < vmin[c] ? xm : vmin[c];
-            stot[c] = stot[c] + s[i];
-          }
-        }
-        col_reduce4_max<NW>(vmax, red[0], L);
-        __syncthreads();
-        col_reduce4_min<NW>(vmin, red[1], L);
-        __syncthreads();
-        col_reduce4<NW>(stot, red[0], L);
-        __syncthreads();
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          const int gmax = vmax[c] > 0.0f ? (int)fminf(ceilf(vmax[c] * scale), scale) : 0;
-          const int gmin = vmin[c] > 0.0f ? (int)fminf(ceilf(vmin[c] * scale), scale + 1.0f) : 0;
-          int lo_c = gmin >= 2 ? gmin - 1 : 0;
-          int hi_c = gmax < 1 ? 1 : gmax;
-          if (lo_c > 0 && !(stot[c] > kappa)) {
-            lo_c = 0;
-            hi_c = 1;
-          }
-          if (lo_c >= top) {
-            lo_c = top - 1;
-            hi_c = top;
-          }
-          if (hi_c <= lo_c) hi_c = lo_c + 1;
-          lo_k[c] = lo_c;
-          hi_k[c] = hi_c;
-        }
-      }
-      for (int it = 0;; ++it) {
-        bool active = false;
-#pragma unroll
-        for (int c = 0; c < 4; ++c) active |= (hi_k[c] - lo_k[c]) > 1;
-        if (!__syncthreads_or(active)) break;
-        float part[4], midf[4];
-        int mid[4];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          mid[c] = (lo_k[c] + hi_k[c]) >> 1;
-          midf[c] = (float)mid[c] * inv_scale;
-          part[c] = 0.0f;
-        }
-#pragma unroll
-        for (int i = 0; i < R; ++i) {
-          const float zs = 0.0f * s[i];
-#pragma unroll
-          for (int c = 0; c < 4; ++c) part[c] = part[c] + ((wn[i][c] > midf[c]) ? s[i] : zs);
-        }
-        col_reduce4<NW>(part, red[it & 1], L);
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          if (hi_k[c] - lo_k[c] > 1) {
-            if (part[c] > kappa)
-              lo_k[c] = mid[c];
-            else
-              hi_k[c] = mid[c];
-          }
-        }
-      }
-      __syncthreads();
-      // C_raw = k 2^-n (exact); tile partial of sum C in a fixed order
-      double cr[4];
-#pragma unroll
-      for (int c = 0; c < 4; ++c) cr[c] = (double)hi_k[c] / (double)top;
-      if (L.g == 0) {
-#pragma unroll
-        for (int c = 0; c < 4; ++c)
-          if (m + c < M) A.craw[slice * M + m + c] = cr[c];
-      }
-      if (rust) {
-        double t = 0.0;
-#pragma unroll
-        for (int c = 0; c < 4; ++c)
-          if (m + c < M) t = t + cr[c];
-        for (int o = 1; o < 16; o <<= 1) t = t + __shfl_xor(t, o, 64);
-        if (threadIdx.x == 0) st_sc1(&A.cpart_d[ls * T + tile], t);
-      } else {
-        float t = 0.0f;
-#pragma unroll
-        for (int c = 0; c < 4; ++c)
-          if (m + c < M) t = t + (float)cr[c];
-        t = sum_row16(t);
-        if (threadIdx.x == 0) st_sc1(&A.cpart_f[ls * T + tile], t);
-      }
-      if (arrive(&sy[2], &sh_u) == (unsigned)(T - 1)) {
-        acquire_block();
-        if (threadIdx.x < 64) {  // wave 0: lane-strided partial sums, then a butterfly
-          if (rust) {
-            double a = 0.0;
-            for (int k = threadIdx.x; k < T; k += 64) a = a + ld_sc1(&A.cpart_d[ls * T + k]);
-            a = wave_sum_d(a);
-            if (threadIdx.x == 0) st_sc1(&A.sumc_d[ls], a);
-          } else {
-            float a = 0.0f;
-            for (int k = threadIdx.x; k < T; k += 64) a = a + ld_sc1(&A.cpart_f[ls * T + k]);
-            a = wave_sum(a);
-            if (threadIdx.x == 0) st_sc1(&A.sumc_f[ls], a);
-          }
-        }
-        raise_flag(&sy[3]);
-      }
-      wait_flag(&sy[3], timeout);
-      // quantise own columns (yumas.py:211; YumaRust :97 in fp64)
-      float Cc[4];
-      if (rust) {
-        const double sc = ld_sc1(&A.sumc_d[ls]);
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          const int lev = (int)(cr[c] / sc * 65535.0);
-          Cc[c] = level_value(lev);
-          if (L.g == 0 && m + c < M) A.qlev[slice * M + m + c] = lev;
-        }
-      } else {
-        const float sc = ld_sc1(&A.sumc_f[ls]);
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          const int lev = (int)((float)cr[c] / sc * 65535.0f);
-          Cc[c] = level_value(lev);
-          if (L.g == 0 && m + c < M) A.qlev[slice * M + m + c] = lev;
-        }
-      }
-#pragma unroll
-      for (int c = 0; c < 4; ++c)
-        if (m + c >= M) Cc[c] = 0.0f;
-      if (L.g == 0)
-#pragma unroll
-        for (int c = 0; c < 4; ++c)
-          if (m + c < M) A.C[slice * M + m + c] = Cc[c];
-
-      // ---- clip + rank (yumas.py:214-217) and the full-output extras
-      float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-      for (int i = 0; i < R; ++i) {
-        const int row = L.g + G * i;
-        float wc[4];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          wc[c] = tmin(wn[i][c], Cc[c]);
-          acc[c] = acc[c] + s[i] * wc[c];
-        }
-        if (row < V) {
-          const long long off = slice * (long long)V * M + (long long)row * M;
-          if (A.Wn_out != nullptr) store4<VEC>(A.Wn_out + off, m, M, wn[i]);
-          if (A.Wc_out != nullptr) store4<VEC>(A.Wc_out + off, m, M, wc);
-        }
-        if (A.tvc != nullptr) {
-          float a = 0.0f, b = 0.0f;
-#pragma unroll
-          for (int c = 0; c < 4; ++c)
-            if (m + c < M) {
-              a = a + wc[c];
-              b = b + wn[i][c];
-            }
-          a = sum_row16(a);
-          b = sum_row16(b);
-          if (L.c4 == 0 && row < V) {
-            A.tvc[(slice * T + tile) * V + row] = a;
-            A.tvn[(slice * T + tile) * V + row] = b;
-          }
-        }
-      }
-      col_reduce4<NW>(acc, red[0], L);
-      if (L.g == 0)
-#pragma unroll
-        for (int c = 0; c < 4; ++c)
-          if (m + c < M) A.R[slice * M + m + c] = acc[c];
-      float ts = 0.0f;
-#pragma unroll
-      for (int c = 0; c < 4; ++c) ts = ts + acc[c];
-      ts = sum_row16(ts);
-      if (threadIdx.x == 0) A.rpart[slice * T + tile] = ts;
-      __syncthreads();
-    }
-    (void)shd;
+// fault[0] |= the fused kernel's timeout word (sticky over the chunks of a run)
+// fault[2..3] += the sweeps that had to poll and their polls (diagnostics)
+__global__ void k_fault(const unsigned* __restrict__ ctl, unsigned* __restrict__ fault) {
+  if (threadIdx.x == 0) {
+    if (ctl[1] != 0u) fault[0] = 1u;
+    fault[2] += ctl[2];
+    fault[3] += ctl[3];
   }
 }
 
@@ -2207,7 +2418,7 @@ __global__ __launch_bounds__(NT) void k_bonds(BondArgs A) {
 // (a register ring refilled as each epoch is consumed), so the per-epoch HBM
 // latency is hidden behind P-1 epochs of work.
 // ---------------------------------------------------------------------------
-template <int VARIANT, int R, bool VEC, int P, bool NTS, bool VECI = false>
+template <int VARIANT, int R, bool VEC, int P, bool VECI>
 __global__ __launch_bounds__(256) void k_bonds_elem(BondArgs A) {
   constexpr int G = 16;
   const Lay L = lay();
@@ -2321,17 +2532,8 @@ __global__ __launch_bounds__(256) void k_bonds_elem(BondArgs A) {
             B[i][c] = tmin(nb, 1.0f);
           }
         }
-        if (A.B_hist != nullptr && row < V) {
-          float* dst = A.B_hist + slice * VM + (long long)row * M;
-          if (NTS && VEC) {
-            // written once, read by nobody in this run: keep it out of L2/MALL
-            if (m < M)
-              __builtin_nontemporal_store(fvec4{B[i][0], B[i][1], B[i][2], B[i][3]},
-                                          reinterpret_cast<fvec4*>(dst + m));
-          } else {
-            store4<VEC>(dst, m, M, B[i]);
-          }
-        }
+        if (A.B_hist != nullptr && row < V)
+          store4<VEC>(A.B_hist + slice * VM + (long long)row * M, m, M, B[i]);
         float d = 0.0f;
 #pragma unroll
         for (int c = 0; c < 4; ++c)
@@ -2351,224 +2553,6 @@ __global__ __launch_bounds__(256) void k_bonds_elem(BondArgs A) {
 }
 
 // ---------------------------------------------------------------------------
-// Phase 2 with the rank folded in (Yuma3 yumas.py:439-475, Yuma4 :533-590;
-// run outputs only, V <= 256). A block owns every validator row of a
-// 16-miner column strip (thread = 1 row x 4 miners, 16 rows per wave), so the
-// rank column sum R[m] = sum_v S W_clipped (yumas.py:442) is a block-local
-// reduction over the W tile the bond update already holds in registers, and
-// the separate rank pass (a whole extra read of W) disappears.
-//   D needs I = R / R.sum() (yumas.py:445), and R.sum() spans every strip, so
-// the strip accumulates sum_m B[v,m] R[m] instead and k_finalize divides by
-// R.sum() once (sum_m B I = (sum_m B R) / R.sum(), the same quantity up to
-// fp32 rounding of the reassociation; the 1e-5 tolerance of the north star).
-//   Epochs go in groups of P (the prefetch ring depth): each epoch's partials
-// S*min(W, C) go to LDS ([epoch][miner][row], padded), then per group one
-// barrier, a fixed-order reduction (wave w takes (epoch, miner) pairs w,
-// w + nw, ...: rows lane + 64j sequentially, then the 64-lane butterfly), a
-// second barrier, and the group's dividend partials from the bond states kept
-// in registers. Two barriers per P epochs keep the waves loosely coupled; the
-// prefetch ring stays in flight across them (no vmcnt drain at a barrier).
-// ---------------------------------------------------------------------------
-constexpr int kRankTileM = 16;  // miners per column strip
-constexpr int kRankLdsV = 260;  // padded row stride of the partial tile (banks)
-constexpr int kRankP = 4;       // prefetch depth (epochs in flight)
-
-// G: epochs per group (barrier pair), a multiple of the ring depth P
-template <int VARIANT, bool VEC, int P, int G>
-__global__ __launch_bounds__(1024) void k_bonds_rank(BondArgs A) {
-  static_assert(G % P == 0, "group = whole ring turns");
-  __shared__ float part[G][kRankTileM][kRankLdsV];
-  __shared__ __align__(16) float rsh[G][kRankTileM];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  const int q = lane & 3;
-  const int row = wave * 16 + (lane >> 2);
-  // XCD-aware order: blocks b and b + 8 share an XCD (round-robin dispatch),
-  // so give each XCD a contiguous run of strips. A 16-miner strip row is half
-  // a 128-B line; its neighbour strip then sits in the same L2, and the two
-  // halves of every W line / bond-history line meet there instead of being
-  // fetched (or partially written) by two different XCDs.
-  int blk = blockIdx.x;
-  if ((gridDim.x & 7) == 0) blk = (blk & 7) * (gridDim.x >> 3) + (blk >> 3);
-  const int tile = blk % A.tiles;  // A.tiles = ceil(M / 16) here
-  const int n = blk / A.tiles;
-  const int N = A.N, V = A.V, M = A.M;
-  const long long VM = (long long)V * M;
-  const int m = tile * kRankTileM + q * 4;
-  const int rr = min(row, V - 1);
-  const bool live = row < V;
-  const unsigned lmask = live ? 0xffffffffu : 0u;
-  const yuma_params_t& pg = A.prm[n];
-  const bool liquid = pg.liquid_mode != YUMA_LIQUID_OFF;
-  const int reset_mode = pg.reset_mode, reset_epoch = pg.reset_epoch, reset_index = pg.reset_index;
-  const float p_bond_alpha = pg.bond_alpha, p_omba = pg.one_minus_bond_alpha;
-  const float p_maxint = pg.maxint, p_capacity_alpha = pg.capacity_alpha, p_decay_keep = pg.decay_keep;
-  // the reset test reads the previous epoch's consensus of one miner; it is
-  // known before the scan (phase 1 is done), so read it once here
-  bool reset_fire = false;
-  if (reset_mode != YUMA_RESET_NONE && reset_epoch >= A.t0 && reset_epoch < A.t1 &&
-      reset_index >= 0 && reset_index < M) {
-    reset_fire = reset_mode == YUMA_RESET_ALWAYS;
-    if (reset_mode == YUMA_RESET_IF_ZERO_CONSENSUS && reset_epoch >= 1)
-      reset_fire = A.C[((long long)(reset_epoch - 1) * N + n) * M + reset_index] == 0.0f;
-  }
-  const int reset_c = reset_index - m;  // column of this thread hit by a reset
-
-  float B[4];
-  bool has_old;
-  {
-    const float* src = A.t0 == 0 ? A.B_init : A.Bstate;
-    has_old = src != nullptr;
-    if (has_old)
-      load4c<VEC>(src + n * VM, rr, V, m, M, B);
-    else
-#pragma unroll
-      for (int c = 0; c < 4; ++c) B[c] = 0.0f;
-  }
-  // retire the bond-state load before the ring is filled (an s_waitcnt the
-  // compiler's waitcnt pass knows about: vmcnt(0)); otherwise its pending
-  // score survives the loop back-edge and every epoch would wait vmcnt(0)
-  __builtin_amdgcn_s_waitcnt(0x0F70);
-
-  float rw[P][4], rd[P], rsn[P], rc[P][4], rba[P][4];
-  auto fetch = [&](int k, int t) {
-    const long long slice = (long long)t * N + n;
-    load4c<VEC>(A.W + slice * VM, rr, V, m, M, rw[k]);
-    rd[k] = A.rsd[slice * V + rr];
-    rsn[k] = A.sn[slice * V + rr];
-    load4c<VEC>(A.C + slice * M, 0, 1, m, M, rc[k]);
-    if (liquid) load4c<VEC>(A.ba + slice * M, 0, 1, m, M, rba[k]);
-  };
-  // Every ring load is unconditional (epochs past the end re-read the last
-  // one): a load on only some paths into the loop header makes the waitcnt
-  // pass assume the shortest history and wait vmcnt(0) every epoch.
-#pragma unroll
-  for (int k = 0; k < P; ++k) fetch(k, min(A.t0 + k, A.t1 - 1));
-
-  float Bk[G][4];  // bond state after each epoch of the group
-  // epoch t = (group base) + k, its inputs in ring slot k % P
-  auto step = [&](int k, int t) {
-    const int sl = k % P;
-    const long long slice = (long long)t * N + n;
-    if (has_old && reset_fire && t == reset_epoch)
-#pragma unroll
-      for (int c = 0; c < 4; ++c) B[c] = (c == reset_c) ? 0.0f : B[c];
-    float wn[4];
-    {
-      const RowDiv rdv = row_div(rd[sl]);
-      bool slow = false;
-#pragma unroll
-      for (int c = 0; c < 4; ++c) wn[c] = div_fast(rw[sl][c], rdv, slow);
-      if (__any(slow)) {
-#pragma unroll
-        for (int c = 0; c < 4; ++c) wn[c] = rw[sl][c] / rd[sl];
-      }
-    }
-    // rank partials S * min(W, C) (yumas.py:439-442); rows >= V add 0 (a bit
-    // mask, not a branch)
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const float x = rsn[sl] * vmin(wn[c], rc[sl][c]);
-      part[k][q * 4 + c][row] = __uint_as_float(__float_as_uint(x) & lmask);
-    }
-    if (VARIANT == YUMA_VARIANT_YUMA3) {
-      const float cap = rsn[sl] * p_maxint;
-      const float ca = p_capacity_alpha * cap;
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const float rem = vmax(cap - B[c], 0.0f);
-        const float pc = vmin(ca, rem);
-        const float nb = p_decay_keep * B[c] + pc * wn[c];
-        B[c] = vmin(nb, cap);
-      }
-    } else {
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const float bac = liquid ? rba[sl][c] : p_bond_alpha;
-        const float omba = liquid ? 1.0f - rba[sl][c] : p_omba;
-        const float bd = B[c] * omba;
-        const float rem = vmax(1.0f - bd, 0.0f);
-        const float nb = bd + vmin(bac * wn[c], rem);
-        B[c] = vmin(nb, 1.0f);
-      }
-    }
-    if (A.B_hist != nullptr && live)
-      store4<VEC>(A.B_hist + slice * VM + (long long)row * M, m, M, B);
-    has_old = true;
-#pragma unroll
-    for (int c = 0; c < 4; ++c) Bk[k][c] = B[c];
-  };
-  // after the kn epochs of a group from tb: R, dividend partials, strip sums
-  auto finish = [&](int kn, int tb) {
-    __syncthreads();  // LDS only: the compiler emits lgkmcnt(0) + s_barrier
-    // wave w reduces (epoch, miner) pairs w, w + nw, ...
-    for (int j = wave; j < kn * kRankTileM; j += nw) {
-      const int k = j / kRankTileM, mm = j % kRankTileM;
-      float a = 0.0f;
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        if (lane + 64 * i < V) a = a + part[k][mm][lane + 64 * i];
-      a = wave_sum(a);
-      if (lane == 0) {
-        rsh[k][mm] = a;
-        const int mg = tile * kRankTileM + mm;
-        if (mg < M) A.R[((long long)(tb + k) * N + n) * M + mg] = a;
-      }
-    }
-    __syncthreads();
-    // dividend partials sum_m B R over the strip
-#pragma unroll
-    for (int k = 0; k < G; ++k) {
-      if (k < kn) {
-        const long long sp = (long long)(tb + k) * N + n;
-        const float4 r4 = *reinterpret_cast<const float4*>(&rsh[k][q * 4]);
-        const float rv[4] = {r4.x, r4.y, r4.z, r4.w};
-        float d = 0.0f;
-#pragma unroll
-        for (int c = 0; c < 4; ++c)
-          if (m + c < M) d = d + Bk[k][c] * rv[c];
-        d = d + __shfl_xor(d, 1, 64);
-        d = d + __shfl_xor(d, 2, 64);
-        if (q == 0 && live) A.dpart[(sp * A.tiles + tile) * V + row] = d;
-      }
-    }
-    // the strip's rank sums (16 miners, fixed butterfly)
-    if (wave == 0) {
-#pragma unroll
-      for (int k0 = 0; k0 < G; k0 += 4) {
-        const int k = k0 + (lane >> 4), mm = lane & 15;
-        float s = (k < kn && tile * kRankTileM + mm < M) ? rsh[k][mm] : 0.0f;
-        s = s + __shfl_xor(s, 1, 64);
-        s = s + __shfl_xor(s, 2, 64);
-        s = s + __shfl_xor(s, 4, 64);
-        s = s + __shfl_xor(s, 8, 64);
-        if (mm == 0 && k < kn) A.rpart[((long long)(tb + k) * N + n) * A.tiles + tile] = s;
-      }
-    }
-  };
-
-  int tb = A.t0;
-  for (; tb + G <= A.t1; tb += G) {
-#pragma unroll
-    for (int k = 0; k < G; ++k) {
-      step(k, tb + k);
-      fetch(k % P, min(tb + k + P, A.t1 - 1));
-    }
-    finish(G, tb);
-  }
-  if (tb < A.t1) {  // the last partial group
-    const int kn = A.t1 - tb;
-#pragma unroll
-    for (int k = 0; k < G; ++k)
-      if (k < kn) {
-        step(k, tb + k);
-        fetch(k % P, min(tb + k + P, A.t1 - 1));
-      }
-    finish(kn, tb);
-  }
-  if (live) store4<VEC>(A.Bstate + n * VM + (long long)row * M, m, M, B);
-}
-
-// ---------------------------------------------------------------------------
 // Finalize, one block per slice: D = sum over tiles of the partials (Yuma4:
 // D = S * that, yumas.py:590), D_normalized = D / (D.sum() + 1e-6), and
 // validator trust T_v = sum Wc / sum W (yumas.py:224).
@@ -2579,8 +2563,7 @@ __global__ __launch_bounds__(256) void k_finalize(const float* __restrict__ dpar
                                                   const float* __restrict__ tvc,
                                                   const float* __restrict__ tvn,
                                                   float* __restrict__ Dn, float* __restrict__ D,
-                                                  float* __restrict__ Tv,
-                                                  const float* __restrict__ rdiv_scal = nullptr) {
+                                                  float* __restrict__ Tv) {
   // thread (tg, vq): tile group tg = tid / 64 sums tiles tg, tg+4, ...; vq owns
   // validators 4vq..4vq+3 of the current 256-validator window. Fixed order:
   // per-group sequential, then groups 0..3.
@@ -2609,12 +2592,6 @@ __global__ __launch_bounds__(256) void k_finalize(const float* __restrict__ dpar
         d = d + part[1][j];
         d = d + part[2][j];
         d = d + part[3][j];
-        if (rdiv_scal != nullptr) {
-          // k_bonds_rank partials are sum_m B R: divide by R.sum() once. I =
-          // nan_to_num(R / R.sum()) is all zero when R.sum() is 0 or not finite
-          const float sr = rdiv_scal[slice * 8 + 5];
-          d = (sr == 0.0f || !isfinite(sr)) ? 0.0f : d / sr;
-        }
         if (variant == YUMA_VARIANT_YUMA4) d = sn[slice * V + v] * d;
         dsh[v] = d;
       }
@@ -2751,8 +2728,9 @@ int fail(int code, const char* fmt, ...) {
 size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
 struct Workspace {
+  unsigned* fault;  // [4] at offset 0: [0] a fused-phase-1 sweep timed out (sticky per run)
   float* rsd;
-  int* sx;  // per slice: exact stake units or -1 (k_rowsum)
+  int* sx;  // per slice: exact stake units or -1 (k_rowsum / k_fused1)
   float* sn;
   double* craw;
   int* qlev;
@@ -2766,22 +2744,29 @@ struct Workspace {
   float* tvc;
   float* tvn;
   float* Bstate;
-  unsigned* sync;   // fused phase 1: per-slice counters/flags + head + timeout
-  size_t sync_bytes;
-  double* cpart_d;
-  float* cpart_f;
   float* sumc_f;
   double* sumc_d;
+  unsigned* f1;     // fused phase 1: ctl[4], then the granule rings (memset per launch)
+  size_t f1_bytes;  // bytes reserved for ctl + rings
   size_t bytes;
 };
 
-// YUMA_RANKFUSE=1: fold the rank pass into the Yuma3/4 bond scan (k_bonds_rank)
-bool rankfuse_knob() {
-  const char* rf = getenv("YUMA_RANKFUSE");
-  return rf != nullptr && rf[0] == '1';
+// Granule rings of k_fused1 for G groups of T blocks (G * T <= kF1MaxBlocks).
+struct F1Rings {
+  size_t rowpart, rowsum, cpart, total;  // byte offsets from ws.f1, total bytes
+};
+F1Rings f1_rings(int G, int T, int V) {
+  F1Rings r{};
+  const size_t slots = (size_t)G * yk::kF1Ring;
+  r.rowpart = 64;  // after ctl[4] (padded)
+  r.rowsum = r.rowpart + slots * T * V * 8;
+  r.cpart = r.rowsum + slots * V * 8;
+  r.total = (r.cpart + slots * T * 2 * 8 + 15) & ~size_t(15);
+  return r;
 }
 
 Workspace carve(char* base, int variant, int N, int E, int V, int M, int full) {
+  (void)variant;
   Workspace w{};
   const size_t S = (size_t)E * N;
   const size_t tiles = (size_t)(M + yk::kTileM - 1) / yk::kTileM;
@@ -2791,6 +2776,7 @@ Workspace carve(char* base, int variant, int N, int E, int V, int M, int full) {
     off += align256(bytes);
     return p;
   };
+  w.fault = (unsigned*)take(16);
   w.rsd = (float*)take(S * V * 4);
   w.sx = (int*)take(S * 4);
   w.sn = (float*)take(S * V * 4);
@@ -2800,22 +2786,22 @@ Workspace carve(char* base, int variant, int N, int E, int V, int M, int full) {
   w.R = (float*)take(S * M * 4);
   w.I = (float*)take(S * M * 4);
   w.ba = (float*)take(S * M * 4);
-  // k_bonds_rank (Yuma3/4, run outputs) keeps per-16-miner-strip partials
-  const size_t ptiles = (rankfuse_knob() && variant >= YUMA_VARIANT_YUMA3 && !full && V <= 256)
-                            ? (size_t)(M + yk::kRankTileM - 1) / yk::kRankTileM
-                            : tiles;
-  w.rpart = (float*)take(S * ptiles * 4);
-  w.dpart = (float*)take(S * ptiles * V * 4);
+  w.rpart = (float*)take(S * (size_t)((M + yk::kF1Tile - 1) / yk::kF1Tile) * 4);
+  w.dpart = (float*)take(S * tiles * V * 4);
   w.scal = (float*)take(S * 8 * 4);
   w.tvc = full ? (float*)take(S * tiles * V * 4) : nullptr;
   w.tvn = full ? (float*)take(S * tiles * V * 4) : nullptr;
   w.Bstate = (float*)take((size_t)N * V * M * 4);
-  w.sync_bytes = ((S * 4 + 4) * 4 + 15) & ~size_t(15);
-  w.sync = (unsigned*)take(w.sync_bytes);
-  w.cpart_d = (double*)take(S * tiles * 8);
-  w.cpart_f = (float*)take(S * tiles * 4);
   w.sumc_f = (float*)take(S * 4);
   w.sumc_d = (double*)take(S * 8);
+  // rings sized for the largest group count any grid of kF1MaxBlocks can form
+  w.f1_bytes = 0;
+  const size_t ftiles = (size_t)(M + yk::kF1Tile - 1) / yk::kF1Tile;
+  if (V <= 256 && ftiles <= (size_t)yk::kF1MaxBlocks) {
+    const int T = (int)ftiles;
+    w.f1_bytes = f1_rings(yk::kF1MaxBlocks / T, T, V).total;
+  }
+  w.f1 = w.f1_bytes ? (unsigned*)take(w.f1_bytes) : nullptr;
   w.bytes = off;
   return w;
 }
@@ -2834,23 +2820,12 @@ RowCfg row_cfg(int V) {
 #define YK_LAUNCH(kernel, grid, block, stream, ...) \
   hipLaunchKernelGGL(kernel, dim3(grid), dim3(block), 0, (hipStream_t)(stream), __VA_ARGS__)
 
-// YUMA_CHIST=0 turns the exact-stake histogram finish of the consensus
-// search off (A/B knob); it is on by default.
-bool chist_knob() {
-  const char* e = getenv("YUMA_CHIST");  // read per launch: tests A/B in one process
-  return !(e != nullptr && !strcmp(e, "0"));
-}
-
 template <int R, bool VEC>
 void launch_consensus_w(long long nblocks, hipStream_t st, const float* W, const float* rsd,
                         const float* sn, const int* sx, const yuma_params_t* prm, int N, int V,
                         int M, long long slice0, int tiles, double* craw, float* P) {
-  if (chist_knob())
-    YK_LAUNCH((yk::k_consensus_w<R, VEC, true>), nblocks, 256, st, W, rsd, sn, sx, prm, N, V, M,
-              slice0, tiles, craw, P);
-  else
-    YK_LAUNCH((yk::k_consensus_w<R, VEC, false>), nblocks, 256, st, W, rsd, sn, sx, prm, N, V,
-              M, slice0, tiles, craw, P);
+  YK_LAUNCH((yk::k_consensus_w<R, VEC>), nblocks, 256, st, W, rsd, sn, sx, prm, N, V, M, slice0,
+            tiles, craw, P);
 }
 
 template <bool VEC>
@@ -2904,35 +2879,6 @@ int device_cus() {
       cus = 1;
   }
   return cus;
-}
-
-template <int NT, int R, bool VEC>
-void launch_phase1_cfg(long long total_items, hipStream_t st, const yk::P1Args& A) {
-  int per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, yk::k_phase1<NT, R, VEC>, NT, 0) !=
-          hipSuccess ||
-      per_cu < 1)
-    per_cu = 1;
-  long long grid = (long long)device_cus() * per_cu;
-  if (grid > total_items) grid = total_items;
-  YK_LAUNCH((yk::k_phase1<NT, R, VEC>), grid, NT, st, A);
-}
-template <bool VEC>
-void launch_phase1(RowCfg rc, long long total_items, hipStream_t st, const yk::P1Args& A) {
-  switch (rc) {
-    case RC_256_1:
-      launch_phase1_cfg<256, 1, VEC>(total_items, st, A);
-      break;
-    case RC_256_4:
-      launch_phase1_cfg<256, 4, VEC>(total_items, st, A);
-      break;
-    case RC_256_16:
-      launch_phase1_cfg<256, 16, VEC>(total_items, st, A);
-      break;
-    case RC_1024_16:
-      launch_phase1_cfg<1024, 16, VEC>(total_items, st, A);
-      break;
-  }
 }
 
 template <bool VEC>
@@ -3007,48 +2953,21 @@ void launch_bonds_colnorm(RowCfg rc, long long nblocks, hipStream_t st, const yk
   }
 }
 
-// Element-wise variants: 256 threads, R rows per thread (R*16 rows per block),
-// inputs of the next kPrefetch epochs kept in flight.
-// YUMA_BONDS=p4|p8|p4nt|p8nt|p4v selects the prefetch depth / history store
-// policy / float4 incentive loads (A/B knob for tools/ab.sh). The default is
-// the measured best on MI355X: 4 epochs in flight, plain stores, and the
-// incentive-load width chosen by whether the bond history is written.
-int bonds_knob() {
-  static int knob = -1;
-  if (knob < 0) {
-    const char* e = getenv("YUMA_BONDS");
-    knob = 0;
-    if (e != nullptr) {
-      if (!strcmp(e, "p8")) knob = 1;
-      else if (!strcmp(e, "p4nt")) knob = 2;
-      else if (!strcmp(e, "p8nt")) knob = 3;
-      else if (!strcmp(e, "p4v")) knob = 4;
-    }
-  }
-  return knob;
-}
+// Element-wise variants: 256 threads, one row x 4 miners per thread (16-row
+// blocks), the inputs of the next 4 epochs kept in flight. Measured on
+// MI355X (c2 / c3): per-column incentive / bond_alpha loads are faster while
+// the bond history is written (1.73 vs 1.92 ms), float4 ones without it
+// (1.11 vs 1.28 ms at c2, 18.0 vs 26.8 ms at c3).
 template <int VARIANT, bool VEC>
-void launch_bonds_elem(int R, long long nblocks, hipStream_t st, const yk::BondArgs& A) {
-  (void)R;
-  switch (bonds_knob()) {
-    case 1: YK_LAUNCH((yk::k_bonds_elem<VARIANT, 1, VEC, 8, false>), nblocks, 256, st, A); break;
-    case 2: YK_LAUNCH((yk::k_bonds_elem<VARIANT, 1, VEC, 4, true>), nblocks, 256, st, A); break;
-    case 3: YK_LAUNCH((yk::k_bonds_elem<VARIANT, 1, VEC, 8, true>), nblocks, 256, st, A); break;
-    case 4: YK_LAUNCH((yk::k_bonds_elem<VARIANT, 1, VEC, 4, false, VEC>), nblocks, 256, st, A); break;
-    default:
-      // measured (MI355X, c2 / c3): per-column incentive / bond_alpha loads
-      // are faster while the bond history is written (1.73 vs 1.92 ms),
-      // float4 ones without it (1.11 vs 1.28 ms at c2, 18.0 vs 26.8 ms at c3)
-      if (A.B_hist == nullptr)
-        YK_LAUNCH((yk::k_bonds_elem<VARIANT, 1, VEC, 4, false, VEC>), nblocks, 256, st, A);
-      else
-        YK_LAUNCH((yk::k_bonds_elem<VARIANT, 1, VEC, 4, false>), nblocks, 256, st, A);
-      break;
-  }
+void launch_bonds_elem(long long nblocks, hipStream_t st, const yk::BondArgs& A) {
+  if (A.B_hist == nullptr)
+    YK_LAUNCH((yk::k_bonds_elem<VARIANT, 1, VEC, 4, VEC>), nblocks, 256, st, A);
+  else
+    YK_LAUNCH((yk::k_bonds_elem<VARIANT, 1, VEC, 4, false>), nblocks, 256, st, A);
 }
 
 template <bool VEC>
-void launch_bonds(int variant, RowCfg rc, int elemR, long long nblocks, hipStream_t st,
+void launch_bonds(int variant, RowCfg rc, long long nblocks, hipStream_t st,
                   const yk::BondArgs& A) {
   switch (variant) {
     case YUMA_VARIANT_RUST:
@@ -3061,27 +2980,12 @@ void launch_bonds(int variant, RowCfg rc, int elemR, long long nblocks, hipStrea
       launch_bonds_colnorm<YUMA_VARIANT_YUMA2, VEC>(rc, nblocks, st, A);
       break;
     case YUMA_VARIANT_YUMA3:
-      launch_bonds_elem<YUMA_VARIANT_YUMA3, VEC>(elemR, nblocks, st, A);
+      launch_bonds_elem<YUMA_VARIANT_YUMA3, VEC>(nblocks, st, A);
       break;
     default:
-      launch_bonds_elem<YUMA_VARIANT_YUMA4, VEC>(elemR, nblocks, st, A);
+      launch_bonds_elem<YUMA_VARIANT_YUMA4, VEC>(nblocks, st, A);
       break;
   }
-}
-
-void launch_bonds_rank(int variant, bool vec, long long nblocks, int threads, hipStream_t st,
-                       const yk::BondArgs& A) {
-  // YUMA_RANKG=4: 4 instead of 8 epochs per barrier pair for Yuma3 (A/B knob)
-  const char* g = getenv("YUMA_RANKG");
-  const bool g4 = g != nullptr && g[0] == '4';
-#define YK_BR(VAR, VEC_, G_) YK_LAUNCH((yk::k_bonds_rank<VAR, VEC_, yk::kRankP, G_>), nblocks, threads, st, A)
-  if (variant == YUMA_VARIANT_YUMA3) {
-    if (g4) { if (vec) YK_BR(YUMA_VARIANT_YUMA3, true, 4); else YK_BR(YUMA_VARIANT_YUMA3, false, 4); }
-    else { if (vec) YK_BR(YUMA_VARIANT_YUMA3, true, 8); else YK_BR(YUMA_VARIANT_YUMA3, false, 8); }
-  } else {  // Yuma4's liquid-alpha ring slots leave no room for 8 bond states
-    if (vec) YK_BR(YUMA_VARIANT_YUMA4, true, 4); else YK_BR(YUMA_VARIANT_YUMA4, false, 4);
-  }
-#undef YK_BR
 }
 
 // Optional per-phase timing (bench / roofline): a HIP event is recorded on the
@@ -3106,61 +3010,29 @@ struct PhaseTimer {
   }
 };
 
-// Second in-order stream for the chunk pipeline (one per device, created on
-// first use, never destroyed: it lives as long as the process).
-hipStream_t aux_stream() {
-  static std::mutex mu;
-  static hipStream_t streams[64] = {};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-  std::lock_guard<std::mutex> g(mu);
-  if (streams[dev] == nullptr &&
-      hipStreamCreateWithFlags(&streams[dev], hipStreamNonBlocking) != hipSuccess)
-    streams[dev] = nullptr;
-  return streams[dev];
+// Which phase-1 path run_impl takes (yuma_set_path; tests compare them).
+int g_path = YUMA_PATH_AUTO;
+
+int fused_blocks() {
+  const int cus = device_cus();
+  return cus < yk::kF1MaxBlocks ? cus : yk::kF1MaxBlocks;
 }
-// st2 waits for everything enqueued on st1 so far (an event edge: also valid
-// inside hipStreamBeginCapture, where it becomes a graph dependency). The
-// events come from a recycled per-device pool: a wait binds to the record
-// that precedes it, so re-recording an event later does not disturb it, and
-// no event is destroyed while work is pending.
-bool stream_edge(hipStream_t st1, hipStream_t st2) {
-  constexpr int kPool = 256;
-  static std::mutex mu;
-  static hipEvent_t pool[64][kPool] = {};
-  static unsigned next[64] = {};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return false;
-  hipEvent_t e;
-  {
-    std::lock_guard<std::mutex> g(mu);
-    hipEvent_t& slot = pool[dev][next[dev]++ % kPool];
-    if (slot == nullptr && hipEventCreateWithFlags(&slot, hipEventDisableTiming) != hipSuccess) {
-      slot = nullptr;
-      return false;
-    }
-    e = slot;
-  }
-  return hipEventRecord(e, st1) == hipSuccess && hipStreamWaitEvent(st2, e, 0) == hipSuccess;
-}
-// Chunk pipeline (opt-in: YUMA_PIPE=k runs k chunks): phase 1a-1c (row sums,
-// consensus, quantisation) of chunk k+1 run on the caller's stream while
-// chunk k's rank, incentive, bond scan and finalize run on the auxiliary
-// stream, to overlap the VALU-bound consensus with the HBM-bound bond scan.
-// Measured slower on MI355X at c2 (5.21 ms at 8 chunks, 5.12 at 4, 5.50 at
-// 16 vs 4.99 unpipelined), so one chunk, one stream by default.
-int pipe_chunks(int E) {
-  static int knob = -2;
-  if (knob == -2) {
-    const char* e = getenv("YUMA_PIPE");
-    knob = e ? atoi(e) : 0;
-  }
-  if (knob <= 0) return 1;
-  const int want = knob;
-  const int minc = 32;  // epochs per chunk below which the bond scan's fill dominates
-  int n = E / minc;
-  if (n > want) n = want;
-  return n < 1 ? 1 : n;
+
+// k_fused1 (opt-in, YUMA_PATH_FUSED) serves run outputs of 32 <= V <= 256
+// validators on float4 rows with whole tile groups resident (T <= one block
+// per CU); Yuma2 (which clips the previous epoch's weights), the full-output
+// dicts of the epoch functions and small subnets take the multi-pass
+// kernels. Measured slower than the multi-pass path at c2 (5.4 vs 2.3 ms for
+// phase 1): one wave per SIMD leaves it VALU-issue
+// bound, and the 128 blocks of a group drift past the hand-offs' lag.
+bool fused_eligible(int variant, int N, int E, int V, int M, bool vec, const yuma_outputs_t* out,
+                    int full) {
+  if (g_path != YUMA_PATH_FUSED) return false;
+  if (!vec || variant == YUMA_VARIANT_YUMA2 || full) return false;
+  if (V < 32 || V > 256 || M < 256) return false;
+  if (out->Wn || out->Wc || out->P || out->T) return false;
+  if ((long long)N * E > (1ll << 30)) return false;  // int slice indices
+  return (M + yk::kF1Tile - 1) / yk::kF1Tile <= fused_blocks();
 }
 
 int run_impl(int variant, const yuma_params_t* prm, int N, int E, int V, int M, const float* W,
@@ -3186,7 +3058,6 @@ int run_impl(int variant, const yuma_params_t* prm, int N, int E, int V, int M, 
   hipStream_t st = (hipStream_t)stream;
   const int tiles = (M + yk::kTileM - 1) / yk::kTileM;
   const RowCfg rc = row_cfg(V);
-  const long long slice_elems = (long long)V * M;
 
   bool vec = (M % 4) == 0 && aligned16(W);
   const float* mats[] = {B_init, Wprev_init, out->Wn, out->Wc, out->Wb, out->B_inst,
@@ -3196,135 +3067,101 @@ int run_impl(int variant, const yuma_params_t* prm, int N, int E, int V, int M, 
 
   float* C = out->C ? out->C : ws.C;
   float* I = out->I ? out->I : ws.I;
+  float* Rr = out->R ? out->R : ws.R;
   float* Bstate = out->B_final ? out->B_final : ws.Bstate;
   // liquid bond_alpha lives in the caller's buffer when requested; scenarios
   // with liquid_mode OFF neither write nor read it
   float* ba_buf = out->bond_alpha ? out->bond_alpha : ws.ba;
+  const bool fused = fused_eligible(variant, N, E, V, M, vec, out, full) && ws.f1 != nullptr;
 
-  if (chunk <= 0 || chunk > E) {
-    // caching a chunk in the 256 MB MALL gains only ~10% on MI355X
-    // (tools/membw: 6.6-7.1 TB/s at 64-256 MB vs 6.44 TB/s from HBM); chunks
-    // exist for the two-stream pipeline (pipe_chunks), not for reuse
-    const int nc = phase_ms != nullptr ? 1 : pipe_chunks(E);
-    chunk = (E + nc - 1) / nc;
-  }
-  (void)slice_elems;
+  // one chunk by default: phase 1 of every epoch, then one bond scan
+  if (chunk <= 0 || chunk > E) chunk = E;
 
-  const int elemR = 1;  // 16-row bond blocks: enough blocks to fill the chip at N = 1
   const int colnorm = variant <= YUMA_VARIANT_YUMA2;
-  const int rowblocks = colnorm ? 1 : (V + 16 * elemR - 1) / (16 * elemR);
-
-  // fused phase 1: not for Yuma2 (clips the previous epoch's weights) and
-  // only while a slice's tiles fit twice into the co-resident blocks
-  // opt-in (YUMA_FUSED=1): measured slower than the multi-pass path on
-  // MI355X (hand-off latency per slice exceeds the saved W reads)
-  const char* fz = getenv("YUMA_FUSED");
-  const bool fused = variant != YUMA_VARIANT_YUMA2 && tiles * 2 <= device_cus() &&
-                     fz != nullptr && fz[0] == '1';
-
-  // rank folded into the bond scan (k_bonds_rank): Yuma3/4 run outputs with
-  // V <= 256 (one block per 16-miner strip holds every row). Small subnets
-  // (M < 64, e.g. the dividend sheet's 3 x 2 cases) keep the separate rank
-  // pass so their reported dividends round exactly as the reference's.
-  // Opt-in (YUMA_RANKFUSE=1): measured slower than the separate rank pass on
-  // MI355X at c2 (rank+bonds 2.72-2.80 ms vs 0.97 + 1.81): a
-  // full-column block forces 16-miner strips, i.e. 64-B row segments.
-  const bool rankfuse = variant >= YUMA_VARIANT_YUMA3 && !full && V <= 256 && M >= 64 &&
-                        out->Wn == nullptr && out->Wc == nullptr && !fused && rankfuse_knob();
-  const int stiles = (M + yk::kRankTileM - 1) / yk::kRankTileM;
+  const int rowblocks = colnorm ? 1 : (V + 15) / 16;
 
   PhaseTimer tm{};
   tm.ms = phase_ms;
   tm.st = st;
-  // st runs phase 1a-1c; sb runs rank .. finalize (the same stream unless
-  // pipelined, see pipe_chunks)
-  hipStream_t sb = st;
-  if (phase_ms == nullptr && chunk < E && !fused) {
-    hipStream_t aux = aux_stream();
-    if (aux != nullptr && stream_edge(st, aux)) sb = aux;
-  }
+  (void)hipMemsetAsync(ws.fault, 0, 16, st);
 
-  for (int c0 = 0, ci = 0; c0 < E; c0 += chunk, ++ci) {
+  for (int c0 = 0; c0 < E; c0 += chunk) {
     const int c1 = c0 + chunk < E ? c0 + chunk : E;
     const long long s0 = (long long)c0 * N;
     const long long ns = (long long)(c1 - c0) * N;
-    const int rowblocks4 = (V + 3) / 4;
     if (fused) {
       tm.mark(YUMA_PHASE_FUSED1);
-      yk::P1Args P{};
-      P.W = W;
-      P.S = S;
-      P.prm = prm;
-      P.N = N;
-      P.V = V;
-      P.M = M;
-      P.tiles = tiles;
-      P.variant = variant;
-      P.slice0 = s0;
-      P.nslices = ns;
-      P.rsd = ws.rsd;
-      P.sn = ws.sn;
-      P.craw = ws.craw;
-      P.C = C;
-      P.qlev = ws.qlev;
-      P.R = out->R ? out->R : ws.R;
-      P.rpart = ws.rpart;
-      P.P = out->P;
-      P.Wn_out = out->Wn;
-      P.Wc_out = out->Wc;
-      P.tvc = ws.tvc;
-      P.tvn = ws.tvn;
-      P.sync = ws.sync;
-      P.rowpart = ws.dpart;  // [ns][tiles][V]: free until the bond phase
-      P.cpart_f = ws.cpart_f;
-      P.cpart_d = ws.cpart_d;
-      P.sumc_f = ws.sumc_f;
-      P.sumc_d = ws.sumc_d;
-      (void)hipMemsetAsync(ws.sync, 0, ws.sync_bytes, st);
-      if (vec)
-        launch_phase1<true>(rc, ns * tiles, st, P);
-      else
-        launch_phase1<false>(rc, ns * tiles, st, P);
+      const int T = (M + yk::kF1Tile - 1) / yk::kF1Tile;
+      long long G = fused_blocks() / T;
+      if (G > ns) G = ns;
+      const F1Rings rg = f1_rings((int)G, T, V);
+      char* f1 = (char*)ws.f1;
+      yk::F1Args A{};
+      A.W = W;
+      A.S = S;
+      A.prm = prm;
+      A.N = N;
+      A.V = V;
+      A.M = M;
+      A.T = T;
+      A.G = (int)G;
+      A.rpb = (V + T - 1) / T;
+      A.nch = (T + 7) / 8;
+      A.rust = variant == YUMA_VARIANT_RUST;
+      A.s0 = (int)s0;
+      A.ns = (int)ns;
+      A.rsd = ws.rsd;
+      A.sn = ws.sn;
+      A.sx = ws.sx;
+      A.C = C;
+      A.qlev = ws.qlev;
+      A.R = Rr;
+      A.rpart = ws.rpart;
+      A.sumc_f = ws.sumc_f;
+      A.sumc_d = ws.sumc_d;
+      A.g_rowpart = (unsigned long long*)(f1 + rg.rowpart);
+      A.g_rowsum = (unsigned long long*)(f1 + rg.rowsum);
+      A.g_cpart = (unsigned long long*)(f1 + rg.cpart);
+      A.ctl = ws.f1;
+      (void)hipMemsetAsync(ws.f1, 0, rg.total, st);  // tickets, tags: re-initialised every launch
+      YK_LAUNCH(yk::k_fused1, G * T, 256, st, A);
+      YK_LAUNCH(yk::k_fault, 1, 64, st, ws.f1, ws.fault);
       tm.mark(YUMA_PHASE_LIQUID);
       YK_LAUNCH(yk::k_liquid<256>, ns, 256, st, prm, N, M, s0, C, ws.qlev, M, ba_buf, ws.scal,
                 ws.sumc_f, ws.sumc_d, variant == YUMA_VARIANT_RUST ? 1 : 0);
-      tm.mark(4);
-      YK_LAUNCH(yk::k_incentive, ns, 256, st, out->R ? out->R : ws.R, ws.rpart, out->P, M, s0,
-                tiles, I, out->P ? out->T : nullptr, ws.scal, nullptr);
     } else {
-    tm.mark(0);
-    if (vec)
-      YK_LAUNCH(yk::k_rowsum<true>, ns * rowblocks4, 256, st, W, S, V, M, s0, rowblocks4,
-                ws.rsd, ws.sn, 0, ws.sx);
-    else
-      YK_LAUNCH(yk::k_rowsum<false>, ns * rowblocks4, 256, st, W, S, V, M, s0, rowblocks4,
-                ws.rsd, ws.sn, 0, ws.sx);
-    tm.mark(1);
-    if (vec)
-      launch_consensus<true>(rc, ns * tiles, st, W, ws.rsd, ws.sn, ws.sx, prm, N, V, M, s0, tiles,
-                             ws.craw, out->P);
-    else
-      launch_consensus<false>(rc, ns * tiles, st, W, ws.rsd, ws.sn, ws.sx, prm, N, V, M, s0, tiles,
-                              ws.craw, out->P);
-    tm.mark(2);
-    YK_LAUNCH(yk::k_quantise<256>, ns, 256, st, ws.craw, prm, variant, N, M, s0, C, ws.qlev,
-              ba_buf, ws.scal, nullptr, nullptr, 0);
-    if (sb != st && !stream_edge(st, sb)) return fail(YUMA_EHIP, "stream edge failed");
-    if (!rankfuse) {
-    tm.mark(3);
-    if (vec)
-      launch_rank<true>(rc, ns * tiles, sb, W, ws.rsd, ws.sn, C, Wprev_init,
-                        variant == YUMA_VARIANT_YUMA2, N, V, M, s0, tiles, out->R ? out->R : ws.R,
-                        ws.rpart, out->Wn, out->Wc, ws.tvc, ws.tvn);
-    else
-      launch_rank<false>(rc, ns * tiles, sb, W, ws.rsd, ws.sn, C, Wprev_init,
-                         variant == YUMA_VARIANT_YUMA2, N, V, M, s0, tiles,
-                         out->R ? out->R : ws.R, ws.rpart, out->Wn, out->Wc, ws.tvc, ws.tvn);
-    tm.mark(4);
-    YK_LAUNCH(yk::k_incentive, ns, 256, sb, out->R ? out->R : ws.R, ws.rpart, out->P, M, s0,
-              tiles, I, out->P ? out->T : nullptr, ws.scal, nullptr);
+      const int rowblocks4 = (V + 3) / 4;
+      tm.mark(YUMA_PHASE_ROWSUM);
+      if (vec)
+        YK_LAUNCH(yk::k_rowsum<true>, ns * rowblocks4, 256, st, W, S, V, M, s0, rowblocks4,
+                  ws.rsd, ws.sn, 0, ws.sx);
+      else
+        YK_LAUNCH(yk::k_rowsum<false>, ns * rowblocks4, 256, st, W, S, V, M, s0, rowblocks4,
+                  ws.rsd, ws.sn, 0, ws.sx);
+      tm.mark(YUMA_PHASE_CONSENSUS);
+      if (vec)
+        launch_consensus<true>(rc, ns * tiles, st, W, ws.rsd, ws.sn, ws.sx, prm, N, V, M, s0, tiles,
+                               ws.craw, out->P);
+      else
+        launch_consensus<false>(rc, ns * tiles, st, W, ws.rsd, ws.sn, ws.sx, prm, N, V, M, s0,
+                                tiles, ws.craw, out->P);
+      tm.mark(YUMA_PHASE_QUANTISE);
+      YK_LAUNCH(yk::k_quantise<256>, ns, 256, st, ws.craw, prm, variant, N, M, s0, C, ws.qlev,
+                ba_buf, ws.scal, nullptr, nullptr, 0);
+      tm.mark(YUMA_PHASE_RANK);
+      if (vec)
+        launch_rank<true>(rc, ns * tiles, st, W, ws.rsd, ws.sn, C, Wprev_init,
+                          variant == YUMA_VARIANT_YUMA2, N, V, M, s0, tiles, Rr, ws.rpart, out->Wn,
+                          out->Wc, ws.tvc, ws.tvn);
+      else
+        launch_rank<false>(rc, ns * tiles, st, W, ws.rsd, ws.sn, C, Wprev_init,
+                           variant == YUMA_VARIANT_YUMA2, N, V, M, s0, tiles, Rr, ws.rpart,
+                           out->Wn, out->Wc, ws.tvc, ws.tvn);
     }
-    }
+    tm.mark(YUMA_PHASE_INCENTIVE);
+    const int rtiles = fused ? (M + yk::kF1Tile - 1) / yk::kF1Tile : tiles;  // rank partials per slice
+    YK_LAUNCH(yk::k_incentive, ns, 256, st, Rr, ws.rpart, out->P, M, s0, rtiles, I,
+              out->P ? out->T : nullptr, ws.scal, nullptr);
 
     yk::BondArgs A{};
     A.W = W;
@@ -3349,39 +3186,23 @@ int run_impl(int variant, const yuma_params_t* prm, int N, int E, int V, int M, 
     A.t0 = c0;
     A.t1 = c1;
     const long long nb = (long long)N * tiles * rowblocks;
-    tm.mark(5);
-    if (rankfuse) {
-      A.tiles = stiles;
-      A.rowblocks = 1;
-      A.R = out->R ? out->R : ws.R;
-      A.rpart = ws.rpart;
-      launch_bonds_rank(variant, vec, (long long)N * stiles, (V + 15) / 16 * 64, sb, A);
-      tm.mark(4);
-      YK_LAUNCH(yk::k_incentive, ns, 256, sb, A.R, ws.rpart, out->P, M, s0, stiles, I,
-                out->P ? out->T : nullptr, ws.scal, nullptr);
-      tm.mark(6);
-      YK_LAUNCH(yk::k_finalize, ns, 256, sb, ws.dpart, ws.sn, variant, V, s0, stiles, ws.tvc,
-                ws.tvn, out->Dn, out->D, out->Tv, ws.scal);
-    } else {
+    tm.mark(YUMA_PHASE_BONDS);
     if (vec)
-      launch_bonds<true>(variant, rc, elemR, nb, sb, A);
+      launch_bonds<true>(variant, rc, nb, st, A);
     else
-      launch_bonds<false>(variant, rc, elemR, nb, sb, A);
-    tm.mark(6);
-    YK_LAUNCH(yk::k_finalize, ns, 256, sb, ws.dpart, ws.sn, variant, V, s0, tiles, ws.tvc,
+      launch_bonds<false>(variant, rc, nb, st, A);
+    tm.mark(YUMA_PHASE_FINALIZE);
+    YK_LAUNCH(yk::k_finalize, ns, 256, st, ws.dpart, ws.sn, variant, V, s0, tiles, ws.tvc,
               ws.tvn, out->Dn, out->D, out->Tv);
-    }
     if (out->Sn != nullptr)
       (void)hipMemcpyAsync(out->Sn + s0 * V, ws.sn + s0 * V, (size_t)ns * V * 4,
-                           hipMemcpyDeviceToDevice, sb);
+                           hipMemcpyDeviceToDevice, st);
     if (out->alpha_ab != nullptr)
       (void)hipMemcpy2DAsync(out->alpha_ab + s0 * 2, 2 * sizeof(float), ws.scal + s0 * 8 + 1,
                              8 * sizeof(float), 2 * sizeof(float), (size_t)ns,
-                             hipMemcpyDeviceToDevice, sb);
+                             hipMemcpyDeviceToDevice, st);
     tm.mark(-1);  // end of chunk
   }
-  // join: the caller's stream sees every output
-  if (sb != st && !stream_edge(sb, st)) return fail(YUMA_EHIP, "stream join failed");
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(YUMA_EHIP, "HIP launch failed: %s", hipGetErrorString(e));
   if (phase_ms != nullptr) {
@@ -3395,7 +3216,7 @@ int run_impl(int variant, const yuma_params_t* prm, int N, int E, int V, int M, 
       (void)hipEventElapsedTime(&t, tm.ev[i], tm.ev[i + 1]);
       if (tm.label[i] >= 0 && tm.label[i] < YUMA_NUM_PHASES) phase_ms[tm.label[i]] += t;
     }
-    for (auto& e : tm.ev) (void)hipEventDestroy(e);
+    for (auto& ev : tm.ev) (void)hipEventDestroy(ev);
   }
   return YUMA_OK;
 }
@@ -3516,9 +3337,9 @@ int shard_stage_impl(int stage, int variant, const yuma_params_t* prm, int N, in
       A.t1 = E;
       const long long nb = (long long)N * tiles * A.rowblocks;
       if (vec)
-        launch_bonds<true>(variant, rc, 1, nb, st, A);
+        launch_bonds<true>(variant, rc, nb, st, A);
       else
-        launch_bonds<false>(variant, rc, 1, nb, st, A);
+        launch_bonds<false>(variant, rc, nb, st, A);
       YK_LAUNCH(yk::k_dsum, ns, 256, st, ws.dpart, V, tiles, io->dsum_part);
       break;
     }
@@ -3654,6 +3475,29 @@ int yuma_graph_destroy(yuma_graph_t graph) {
   (void)hipGraphDestroy(graph->graph);
   delete graph;
   return YUMA_OK;
+}
+
+int yuma_set_path(int path) {
+  if (path != YUMA_PATH_AUTO && path != YUMA_PATH_MULTIPASS && path != YUMA_PATH_FUSED)
+    return fail(YUMA_EINVAL, "unknown path %d", path);
+  const int prev = g_path;
+  g_path = path;
+  return prev;
+}
+
+int yuma_workspace_counters(const void* workspace, unsigned* out4) {
+  if (workspace == nullptr || out4 == nullptr) return fail(YUMA_EINVAL, "NULL argument");
+  if (hipMemcpy(out4, workspace, 16, hipMemcpyDeviceToHost) != hipSuccess)
+    return fail(YUMA_EHIP, "reading the workspace counters failed");
+  return YUMA_OK;
+}
+
+int yuma_workspace_status(const void* workspace) {
+  if (workspace == nullptr) return fail(YUMA_EINVAL, "NULL workspace");
+  unsigned f = 0;
+  if (hipMemcpy(&f, workspace, sizeof f, hipMemcpyDeviceToHost) != hipSuccess)
+    return fail(YUMA_EHIP, "reading the workspace status failed");
+  return (int)f;
 }
 
 const char* yuma_last_error(void) { return g_err; }

@@ -29,7 +29,9 @@ LIB_PATH = os.environ.get("YUMA_HIP_LIB", os.path.join(_PKG_ROOT, "lib", LIB_NAM
 
 VARIANT_RUST, VARIANT_YUMA1, VARIANT_YUMA2, VARIANT_YUMA3, VARIANT_YUMA4 = range(5)
 PHASES = ("rowsum", "consensus", "quantise", "rank", "incentive", "bonds", "finalize",
-          "phase1_fused", "liquid")
+          "fused1", "liquid")
+FLAG_NO_HIST = 1  # yuma_params_t.flags: plain bisection instead of the histogram finish
+PATH_AUTO, PATH_MULTIPASS, PATH_FUSED = 0, 1, 2
 RESET_NONE, RESET_ALWAYS, RESET_IF_ZERO_CONSENSUS = range(3)
 LIQUID_OFF, LIQUID_QUANTILE, LIQUID_CONST_AB = range(3)
 OVR_HIGH, OVR_LOW, OVR_FORCE_Q99 = 1, 2, 4
@@ -45,6 +47,9 @@ EXPORTED_SYMBOLS = (
     "yuma_graph_launch",
     "yuma_graph_nodes",
     "yuma_graph_destroy",
+    "yuma_set_path",
+    "yuma_workspace_status",
+    "yuma_workspace_counters",
     "yuma_last_error",
     "yuma_version",
 )
@@ -67,7 +72,7 @@ class YumaParamsC(ctypes.Structure):
         ("reset_mode", ctypes.c_int32),
         ("reset_epoch", ctypes.c_int32),
         ("reset_index", ctypes.c_int32),
-        ("reserved0", ctypes.c_int32),
+        ("flags", ctypes.c_int32),
         ("kappa", ctypes.c_float),
         ("bond_penalty", ctypes.c_float),
         ("one_minus_bond_penalty", ctypes.c_float),
@@ -120,7 +125,7 @@ def load_library(path: str | None = None):
     with _lock:
         if _lib is not None:
             return _lib
-        p = path or os.environ.get("YUMA_LIB") or LIB_PATH  # YUMA_LIB: A/B builds (tools/ab_lib.sh)
+        p = path or os.environ.get("YUMA_LIB") or LIB_PATH  # YUMA_LIB: A/B of two builds (tools/ab_lib.sh)
         if not os.path.exists(p):
             raise EngineUnavailable(
                 f"{LIB_NAME} not found at {p}; build it with `python -c 'import __graft_entry__ as g; g.build()'`"
@@ -143,16 +148,21 @@ def load_library(path: str | None = None):
         lib.yuma_shard_stage.restype = i32
         lib.yuma_synth_weights.argtypes = [ctypes.c_uint64, i32, i32, i32, i32, i32, vp, vp]
         lib.yuma_synth_weights.restype = i32
-        if hasattr(lib, "yuma_graph_create"):  # absent only in older A/B builds (YUMA_LIB)
-            lib.yuma_graph_create.argtypes = [ctypes.POINTER(vp), i32, vp, i32, i32, i32, i32, vp, vp,
-                                              vp, vp, vp, vp, sz, i32]
-            lib.yuma_graph_create.restype = i32
-            lib.yuma_graph_launch.argtypes = [vp, vp]
-            lib.yuma_graph_launch.restype = i32
-            lib.yuma_graph_nodes.argtypes = [vp]
-            lib.yuma_graph_nodes.restype = i32
-            lib.yuma_graph_destroy.argtypes = [vp]
-            lib.yuma_graph_destroy.restype = i32
+        lib.yuma_graph_create.argtypes = [ctypes.POINTER(vp), i32, vp, i32, i32, i32, i32, vp, vp,
+                                          vp, vp, vp, vp, sz, i32]
+        lib.yuma_graph_create.restype = i32
+        lib.yuma_graph_launch.argtypes = [vp, vp]
+        lib.yuma_graph_launch.restype = i32
+        lib.yuma_graph_nodes.argtypes = [vp]
+        lib.yuma_graph_nodes.restype = i32
+        lib.yuma_graph_destroy.argtypes = [vp]
+        lib.yuma_graph_destroy.restype = i32
+        lib.yuma_set_path.argtypes = [i32]
+        lib.yuma_set_path.restype = i32
+        lib.yuma_workspace_status.argtypes = [vp]
+        lib.yuma_workspace_status.restype = i32
+        lib.yuma_workspace_counters.argtypes = [vp, ctypes.POINTER(ctypes.c_uint32)]
+        lib.yuma_workspace_counters.restype = i32
         lib.yuma_last_error.argtypes = []
         lib.yuma_last_error.restype = ctypes.c_char_p
         lib.yuma_version.argtypes = []
@@ -413,6 +423,34 @@ def synth_weights(seed: int, E: int, N: int, V: int, M: int, t0: int = 0,
     _check(load_library().yuma_synth_weights(int(seed) & 0xFFFFFFFFFFFFFFFF, E, N, V, M, t0,
                                              out.data_ptr(), stream), "yuma_synth_weights")
     return out
+
+
+def set_path(path: int) -> int:
+    """Phase-1 path for this process: PATH_AUTO / PATH_MULTIPASS (the
+    multi-pass kernels) or PATH_FUSED (the single-read fused kernel where it
+    applies). Returns the previous setting."""
+    rc = load_library().yuma_set_path(int(path))
+    if rc < 0:
+        _check(rc, "yuma_set_path")
+    return rc
+
+
+def workspace_status(result: "RunResult") -> int:
+    """0 when the run that produced `result` completed cleanly; 1 when a
+    fused phase-1 hand-off timed out (its outputs are invalid). Synchronous."""
+    ws = result.extra["_inputs"][5]
+    rc = load_library().yuma_workspace_status(ctypes.c_void_p(ws.data_ptr()))
+    if rc < 0:
+        _check(rc, "yuma_workspace_status")
+    return rc
+
+
+def workspace_counters(ws: torch.Tensor) -> list[int]:
+    """[status, -, fused sweeps that polled, polls] of a workspace (diagnostics)."""
+    buf = (ctypes.c_uint32 * 4)()
+    _check(load_library().yuma_workspace_counters(ctypes.c_void_p(ws.data_ptr()), buf),
+           "yuma_workspace_counters")
+    return list(buf)
 
 
 def version() -> str:
