@@ -64,8 +64,11 @@ enum yuma_override_flags { YUMA_OVR_HIGH = 1, YUMA_OVR_LOW = 2, YUMA_OVR_FORCE_Q
 
 /* yuma_params_t.flags. YUMA_FLAG_NO_HIST: run the consensus search as the
  * plain bisection even where the exact-stake histogram finish applies (both
- * give the same result; tests compare them). */
-enum yuma_flags { YUMA_FLAG_NO_HIST = 1 };
+ * give the same result; tests compare them). YUMA_FLAG_RESET_ALL_COLUMNS: the
+ * reset zeroes every miner column (reset_index ignored) -- the reference's
+ * `B_state[:, None] = 0.0` when reset_bonds_index is None
+ * (simulation_utils.py:63-64). */
+enum yuma_flags { YUMA_FLAG_NO_HIST = 1, YUMA_FLAG_RESET_ALL_COLUMNS = 2 };
 
 /* Per-scenario parameters: the flattened YumaConfig (yumas.py:7-45) with every
  * Python-double constant pre-rounded exactly as the reference's torch ops round
@@ -77,8 +80,8 @@ typedef struct yuma_params {
   int32_t override_flags;   /* yuma_override_flags                                 */
   int32_t reset_mode;       /* yuma_reset_mode                                     */
   int32_t reset_epoch;      /* epoch index of the reset (run_simulation epoch)     */
-  int32_t reset_index;      /* miner column to reset                               */
-  int32_t flags;            /* yuma_flags (test switches; 0 in production)         */
+  int32_t reset_index;      /* miner column to reset, 0 <= reset_index < M         */
+  int32_t flags;            /* yuma_flags                                          */
   float kappa;              /* fp32(kappa)                                         */
   float bond_penalty;       /* fp32(beta)                                          */
   float one_minus_bond_penalty; /* fp32(1 - beta), difference taken in double      */

@@ -244,6 +244,38 @@ def test_run_medium_matches_reference(golden, sname):
         assert_close(np.stack([to_np(x) for x in inc]), g[f"{tag}__I"], what=f"{tag} I")
 
 
+@pytest.mark.parametrize("version", ["Yuma 3.1 (Rhef+reset)", "Yuma 3.2 (Rhef+conditional)",
+                                     "Yuma 4 (Rhef+relative bonds)"])
+def test_reset_index_python_semantics(version):
+    """Negative and None reset_bonds_index as the reference's torch indexing
+    reads them (simulation_utils.py:62-88): -k counts from the end; None zeroes
+    every column for Yuma 3.1 and raises for Yuma 3.2/4 (M > 1). Checked
+    against the oracle, whose numpy indexing has the same semantics."""
+    rng = np.random.default_rng(11)
+    E, V, M = 8, 16, 40
+    W = rng.random((E, V, M), dtype=np.float32)
+    W[:, :, 5:9] *= (rng.random((E, V, 4)) < 0.3)  # columns that reach C == 0
+    W[3:, :, -3] = 0.0  # the reset column has zero consensus before epoch 4 (fires for 3.2/4)
+    S = rng.random((E, V), dtype=np.float32)
+    cfg = Y.YumaConfig(simulation=Y.SimulationHyperparameters(bond_penalty=0.5))
+    neg = run_simulation(ArrayCase(W, S, 4, -3), version, cfg)
+    pos = run_simulation(ArrayCase(W, S, 4, M - 3), version, cfg)
+    for a, b in zip(neg[1], pos[1]):
+        assert torch.equal(a, b)
+    ref = orc.run(version, W, S, cfg, reset_epoch=4, reset_index=-3)
+    assert_close(np.stack([to_np(b) for b in neg[1]]), ref["B"], what=f"{version} B (index -3)")
+    if version.startswith("Yuma 3.1"):
+        allc = run_simulation(ArrayCase(W, S, 4, None), version, cfg)
+        ref = orc.run(version, W, S, cfg, reset_epoch=4, reset_index=None)
+        assert_close(np.stack([to_np(b) for b in allc[1]]), ref["B"], what="3.1 B (index None)")
+        assert not torch.equal(allc[1][4], pos[1][4])
+    else:
+        with pytest.raises(RuntimeError):
+            run_simulation(ArrayCase(W, S, 4, None), version, cfg)
+    with pytest.raises(IndexError):
+        run_simulation(ArrayCase(W, S, 4, M), version, cfg)
+
+
 # ---------------------------------------------------------------------------
 # BASELINE shape 256 x 4096
 # ---------------------------------------------------------------------------

@@ -10,7 +10,7 @@ import torch
 
 from conftest import ROOT
 from yuma_simulation._internal import cases as C
-from yuma_simulation._internal import engine, synth
+from yuma_simulation._internal import engine, wide, synth
 from yuma_simulation._internal import yumas as Y
 from yuma_simulation._internal.simulation_utils import VERSION_TABLE, resolve_version
 
@@ -113,6 +113,42 @@ def test_liquid_override_modes():
 def test_reset_without_metadata_never_fires():
     p = engine.make_params(engine.VARIANT_YUMA3, Y.YumaConfig(), reset_mode=engine.RESET_ALWAYS)
     assert p.reset_mode == engine.RESET_NONE
+
+
+def test_reset_index_follows_python_indexing():
+    """run_simulation indexes B_state[:, idx] / scw[idx] (simulation_utils.py:63-85)."""
+    mk = lambda mode, e, i, M=12, E=8: engine.make_params(
+        engine.VARIANT_YUMA3, Y.YumaConfig(), reset_mode=mode, reset_epoch=e, reset_index=i, n_miners=M, n_epochs=E)
+    p = mk(engine.RESET_ALWAYS, 3, -3)
+    assert (p.reset_mode, p.reset_epoch, p.reset_index, p.flags) == (engine.RESET_ALWAYS, 3, 9, 0)
+    p = mk(engine.RESET_IF_ZERO_CONSENSUS, 3, -12)
+    assert p.reset_index == 0
+    # None: B_state[:, None] = 0.0 zeroes every column (Yuma 3.1) ...
+    p = mk(engine.RESET_ALWAYS, 3, None)
+    assert p.reset_mode == engine.RESET_ALWAYS and p.flags & engine.FLAG_RESET_ALL_COLUMNS
+    # ... while scw[None] == 0.0 has no truth value for M > 1 (Yuma 3.2 / 4)
+    with pytest.raises(RuntimeError):
+        mk(engine.RESET_IF_ZERO_CONSENSUS, 3, None)
+    p = mk(engine.RESET_IF_ZERO_CONSENSUS, 3, None, M=1)
+    assert p.reset_mode == engine.RESET_IF_ZERO_CONSENSUS and p.reset_index == 0 and p.flags == 0
+    for bad in (12, -13):
+        with pytest.raises(IndexError):
+            mk(engine.RESET_ALWAYS, 3, bad)
+    # the statement is never reached at epoch 0 (B_state is None) or past the run
+    for e in (0, 8, -1):
+        assert mk(engine.RESET_ALWAYS, e, 99).reset_mode == engine.RESET_NONE
+        assert mk(engine.RESET_IF_ZERO_CONSENSUS, e, None).reset_mode == engine.RESET_NONE
+    assert mk(engine.RESET_ALWAYS, None, 99).reset_mode == engine.RESET_NONE
+    with pytest.raises(ValueError):  # a negative index cannot be resolved without M
+        engine.make_params(engine.VARIANT_YUMA3, Y.YumaConfig(), reset_mode=engine.RESET_ALWAYS,
+                           reset_epoch=3, reset_index=-1)
+
+
+def test_shard_params_keeps_all_columns_reset():
+    p = engine.make_params(engine.VARIANT_YUMA3, Y.YumaConfig(), reset_mode=engine.RESET_ALWAYS,
+                           reset_epoch=3, reset_index=None, n_miners=300, n_epochs=8)
+    out = [wide.shard_params([p], c)[0] for c in wide.column_ranges(300, 3)]
+    assert all(q.reset_mode == engine.RESET_ALWAYS and q.flags & engine.FLAG_RESET_ALL_COLUMNS for q in out)
 
 
 def test_cases_surface():

@@ -2231,19 +2231,20 @@ __global__ __launch_bounds__(NT) void k_bonds(BondArgs A) {
     const long long slice = (long long)t * N + n;
     // bond resets of run_simulation (simulation_utils.py:62-88), applied to
     // the state before this epoch's update
+    const bool reset_all = (p.flags & YUMA_FLAG_RESET_ALL_COLUMNS) != 0;
     if ((VARIANT == YUMA_VARIANT_YUMA3 || VARIANT == YUMA_VARIANT_YUMA4) && has_old &&
-        p.reset_mode != YUMA_RESET_NONE && t == p.reset_epoch && p.reset_index >= 0 &&
-        p.reset_index < M) {
+        p.reset_mode != YUMA_RESET_NONE && t == p.reset_epoch &&
+        (reset_all || (p.reset_index >= 0 && p.reset_index < M))) {
       bool fire = p.reset_mode == YUMA_RESET_ALWAYS;
-      if (p.reset_mode == YUMA_RESET_IF_ZERO_CONSENSUS && t >= 1)
+      if (p.reset_mode == YUMA_RESET_IF_ZERO_CONSENSUS && t >= 1 && !reset_all)
         fire = A.C[(slice - N) * M + p.reset_index] == 0.0f;
       const int c = p.reset_index - m;
-      if (fire && c >= 0 && c < 4)
+      if (fire && (reset_all || (c >= 0 && c < 4)))
 #pragma unroll
         for (int i = 0; i < R; ++i) {
 #pragma unroll
           for (int cc = 0; cc < 4; ++cc)
-            if (cc == c) B[i][cc] = 0.0f;
+            if (reset_all || cc == c) B[i][cc] = 0.0f;
         }
     }
     float Ic[4], Cc[4], bac[4], omba[4];
@@ -2433,6 +2434,7 @@ __global__ __launch_bounds__(256) void k_bonds_elem(BondArgs A) {
   const yuma_params_t& pg = A.prm[n];
   const bool liquid = pg.liquid_mode != YUMA_LIQUID_OFF;
   const int reset_mode = pg.reset_mode, reset_epoch = pg.reset_epoch, reset_index = pg.reset_index;
+  const bool reset_all = (pg.flags & YUMA_FLAG_RESET_ALL_COLUMNS) != 0;
   const float p_bond_alpha = pg.bond_alpha, p_omba = pg.one_minus_bond_alpha;
   const float p_maxint = pg.maxint, p_capacity_alpha = pg.capacity_alpha, p_decay_keep = pg.decay_keep;
   const int row0 = rb * G * R + L.g;
@@ -2482,18 +2484,18 @@ __global__ __launch_bounds__(256) void k_bonds_elem(BondArgs A) {
       const int t = tb + k;
       if (t >= A.t1) break;
       const long long slice = (long long)t * N + n;
-      if (has_old && reset_mode != YUMA_RESET_NONE && t == reset_epoch && reset_index >= 0 &&
-          reset_index < M) {
+      if (has_old && reset_mode != YUMA_RESET_NONE && t == reset_epoch &&
+          (reset_all || (reset_index >= 0 && reset_index < M))) {
         bool fire = reset_mode == YUMA_RESET_ALWAYS;
-        if (reset_mode == YUMA_RESET_IF_ZERO_CONSENSUS && t >= 1)
+        if (reset_mode == YUMA_RESET_IF_ZERO_CONSENSUS && t >= 1 && !reset_all)
           fire = A.C[(slice - N) * M + reset_index] == 0.0f;
         const int c = reset_index - m;
-        if (fire && c >= 0 && c < 4)
+        if (fire && (reset_all || (c >= 0 && c < 4)))
 #pragma unroll
           for (int i = 0; i < R; ++i)
 #pragma unroll
             for (int cc = 0; cc < 4; ++cc)
-              if (cc == c) B[i][cc] = 0.0f;
+              if (reset_all || cc == c) B[i][cc] = 0.0f;
       }
       float bac[4], omba[4];
 #pragma unroll

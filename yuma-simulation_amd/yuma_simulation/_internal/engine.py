@@ -16,6 +16,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import operator
 import os
 import threading
 from dataclasses import dataclass
@@ -31,6 +32,7 @@ VARIANT_RUST, VARIANT_YUMA1, VARIANT_YUMA2, VARIANT_YUMA3, VARIANT_YUMA4 = range
 PHASES = ("rowsum", "consensus", "quantise", "rank", "incentive", "bonds", "finalize",
           "fused1", "liquid")
 FLAG_NO_HIST = 1  # yuma_params_t.flags: plain bisection instead of the histogram finish
+FLAG_RESET_ALL_COLUMNS = 2  # the reset zeroes every column (reset_bonds_index None)
 PATH_AUTO, PATH_MULTIPASS, PATH_FUSED = 0, 1, 2
 RESET_NONE, RESET_ALWAYS, RESET_IF_ZERO_CONSENSUS = range(3)
 LIQUID_OFF, LIQUID_QUANTILE, LIQUID_CONST_AB = range(3)
@@ -210,7 +212,8 @@ def f32(x) -> float:
 
 
 def make_params(variant: int, config, *, maxint: int = 2**64 - 1, reset_mode: int = RESET_NONE,
-                reset_epoch: int | None = None, reset_index: int | None = None) -> YumaParamsC:
+                reset_epoch: int | None = None, reset_index: int | None = None,
+                n_miners: int | None = None, n_epochs: int | None = None) -> YumaParamsC:
     """Flatten a YumaConfig (yumas.py:29-45) into the engine's POD record."""
     p = YumaParamsC()
     p.variant = variant
@@ -256,12 +259,58 @@ def make_params(variant: int, config, *, maxint: int = 2**64 - 1, reset_mode: in
                 p.const_a, p.const_b = f32(a), f32(b)
                 p.liquid_mode = LIQUID_CONST_AB
         p.override_flags = flags
-    p.reset_mode = reset_mode
-    p.reset_epoch = -1 if reset_epoch is None else int(reset_epoch)
-    p.reset_index = -1 if reset_index is None else int(reset_index)
-    if reset_mode != RESET_NONE and (reset_epoch is None or reset_index is None):
-        p.reset_mode = RESET_NONE  # `epoch == None` never fires in the reference
+    _pack_reset(p, reset_mode, reset_epoch, reset_index, n_miners, n_epochs)
     return p
+
+
+def _pack_reset(p: YumaParamsC, reset_mode: int, reset_epoch, reset_index, n_miners, n_epochs) -> None:
+    """The bond reset of run_simulation (simulation_utils.py:62-88) with the
+    reference's Python indexing: `B_state[:, idx] = 0.0` and
+    `server_consensus_weight[idx] == 0.0`, evaluated only at
+    `epoch == reset_bonds_epoch` once B_state exists (epoch >= 1).
+
+    - reset_epoch None: `epoch == None` is never true, no reset;
+    - negative index: counts from the end (idx % M);
+    - index None: `B_state[:, None]` zeroes every column (Yuma 3.1); Yuma 3.2/4
+      also evaluate `scw[None] == 0.0`, a [1, M] tensor whose truth value
+      raises RuntimeError for M > 1 (for M == 1 it is column 0);
+    - index outside [-M, M): IndexError.
+    The errors are raised only when the reference would reach the statement
+    (reset_epoch in [1, n_epochs)). n_miners is needed for anything but a
+    plain in-range non-negative index."""
+    p.reset_mode = RESET_NONE
+    p.reset_epoch = -1
+    p.reset_index = 0
+    if reset_mode == RESET_NONE or reset_epoch is None:
+        return
+    epoch = int(reset_epoch)
+    reached = epoch >= 1 and (n_epochs is None or epoch < n_epochs)
+    if not reached and n_epochs is not None:
+        return  # the statement never runs
+    if not -2**31 <= epoch < 2**31:
+        return  # beyond any int32 epoch count: never equal
+    if reset_index is None:
+        if n_miners is None:
+            raise ValueError("a reset with reset_bonds_index None needs n_miners")
+        if reset_mode == RESET_IF_ZERO_CONSENSUS and n_miners > 1:
+            raise RuntimeError("Boolean value of Tensor with more than one value is ambiguous "
+                               "(server_consensus_weight[None] == 0.0, simulation_utils.py:72,83)")
+        if reset_mode == RESET_ALWAYS:
+            p.flags |= FLAG_RESET_ALL_COLUMNS
+            idx = 0
+        else:
+            idx = 0  # M == 1: scw[None] is the single column
+    else:
+        idx = operator.index(reset_index)
+        if n_miners is not None:
+            if not -n_miners <= idx < n_miners:
+                raise IndexError(f"index {idx} is out of bounds for dimension 1 with size {n_miners}")
+            idx %= n_miners
+        elif idx < 0:
+            raise ValueError("a negative reset_bonds_index needs n_miners to resolve")
+    p.reset_mode = reset_mode
+    p.reset_epoch = epoch
+    p.reset_index = idx
 
 
 def params_tensor(params: list[YumaParamsC], dev: torch.device) -> torch.Tensor:

@@ -102,7 +102,8 @@ def run_simulations(runs: list[SimulationRun], *, want_bonds: bool = True,
             _, reset_mode, _, _ = packed[k]
             params.append(engine.make_params(variant, r.yuma_config, reset_mode=reset_mode,
                                              reset_epoch=r.case.reset_bonds_epoch,
-                                             reset_index=r.case.reset_bonds_index))
+                                             reset_index=r.case.reset_bonds_index,
+                                             n_miners=M, n_epochs=E))
         W = torch.stack([packed[k][2] for k in idx], dim=1)  # [E, N, V, M]
         S = torch.stack([packed[k][3] for k in idx], dim=1)  # [E, N, V]
         res = engine.run(variant, params, W, S, want_hist=want_bonds)

@@ -54,16 +54,16 @@ def column_ranges(M: int, n_shards: int) -> list[range]:
 def shard_params(params: list, cols: range) -> list:
     """Per-shard copies of the parameter records: the bond-reset column
     (simulation_utils.py:62-88) becomes shard-local, or the reset is dropped
-    on shards that do not own it."""
+    on shards that do not own it; an all-columns reset stays on every shard."""
     out = []
     for p in params:
         q = type(p).from_buffer_copy(bytes(p))
-        if q.reset_mode != engine.RESET_NONE:
+        if q.reset_mode != engine.RESET_NONE and not q.flags & engine.FLAG_RESET_ALL_COLUMNS:
             if q.reset_index in cols:
                 q.reset_index = q.reset_index - cols.start
             else:
                 q.reset_mode = engine.RESET_NONE
-                q.reset_index = -1
+                q.reset_index = 0
         out.append(q)
     return out
 

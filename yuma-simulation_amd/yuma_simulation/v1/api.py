@@ -59,8 +59,13 @@ def generate_chart_table(
     draggable_table: bool = False,
 ) -> HTML:
     table_data: dict[str, list[str]] = {version: [] for version, _ in yuma_versions}
-    configs = [YumaConfig(simulation=yuma_hyperparameters, yuma_params=p) for _, p in yuma_versions]
-    runs = [SimulationRun(case, version, cfg) for case in cases for (version, _), cfg in zip(yuma_versions, configs)]
+    # The reference collects each row as {version: chart} (reference v1/api.py:34-36, 50-119), so
+    # a version listed twice keeps one column, filled by its LAST entry
+    # (that entry's params and title), at the position of its first.
+    last_params = {version: params for version, params in yuma_versions}
+    versions = [(version, last_params[version]) for version in table_data]
+    configs = [YumaConfig(simulation=yuma_hyperparameters, yuma_params=p) for _, p in versions]
+    runs = [SimulationRun(case, version, cfg) for case in cases for (version, _), cfg in zip(versions, configs)]
     results = run_simulations(runs)
     case_row_ranges = []
     row = 0
@@ -69,11 +74,11 @@ def generate_chart_table(
         chart_types = ["weights", "dividends", "bonds", "normalized_bonds"]
         if idx in (9, 10):
             chart_types.append("incentives")
-        per_version = results[k:k + len(yuma_versions)]
-        k += len(yuma_versions)
+        per_version = results[k:k + len(versions)]
+        k += len(versions)
         start = row
         for chart_type in chart_types:
-            for ((version, _), cfg), (dividends, bonds, incentives) in zip(zip(yuma_versions, configs), per_version):
+            for ((version, _), cfg), (dividends, bonds, incentives) in zip(zip(versions, configs), per_version):
                 title = _full_case_name(case, version, cfg)
                 if chart_type == "weights":
                     img = _plot_validator_server_weights(case.validators, case.weights_epochs, case.servers,
