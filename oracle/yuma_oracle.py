@@ -143,6 +143,54 @@ def consensus(Wn: np.ndarray, S: np.ndarray, kappa: float, precision, as_double:
     return hi if as_double else hi.astype(F32)
 
 
+def tie_columns(W, S, kappa: float, precision, as_double: bool = False, ulps: int = 64) -> np.ndarray:
+    """Miner columns whose consensus level depends on summation ORDER, so
+    that two correct fp32 implementations (torch's CPU kernels, this numpy
+    port, the HIP engine) may legitimately disagree on them.
+
+    The reference decides `(W > mid) @ S > kappa` (yumas.py:203-204), sums
+    W's rows (:186) and C (:211) in fp32, in torch's order. A column is
+    flagged when, on the bisection path this oracle takes, either
+      * the exact stake sum lies within V * 2^-24 of fp32(kappa) (the bound
+        on any fp32 summation order of <= V terms in [0, 1]), or
+      * a validator with stake has a normalised weight within `ulps` ulps of
+        the midpoint (the row sums, hence W / rowsum, differ by order);
+    or the quantisation `C / sum(C) * 65535` lies within `ulps` ulps of an
+    integer (sum(C) differs by order). Outside these columns C must be
+    bit-equal. Returns a bool mask [M]."""
+    W = np.asarray(W, F32)
+    S = np.asarray(S, F32)
+    V, M = W.shape
+    rs = W.sum(axis=1, dtype=F32)
+    Wn = (W / (rs + F32(1e-6))[:, None]).astype(F32)
+    Sn = (S / S.sum(dtype=F32)).astype(F32)
+    staked = Sn > 0
+    k32 = np.float64(F32(kappa))
+    win = V * 2.0 ** -24
+    Sc = Sn[:, None]
+    S64 = Sn.astype(np.float64)
+    lo = np.zeros(M, dtype=np.float64)
+    hi = np.ones(M, dtype=np.float64)
+    flag = np.zeros(M, dtype=bool)
+    for _ in range(bisect_iterations(precision)):
+        mid = (hi + lo) / 2.0
+        midf = mid.astype(F32)
+        above = Wn > midf[None, :]
+        exact = (np.where(above, S64[:, None], 0.0)).sum(axis=0)
+        flag |= np.abs(exact - k32) <= win
+        near = np.abs(Wn.astype(np.float64) - midf[None, :]) <= ulps * np.spacing(midf)[None, :]
+        flag |= (near & staked[:, None]).any(axis=0)
+        sums = np.where(above, Sc, F32(0.0)).sum(axis=0, dtype=F32)
+        up = sums > F32(kappa)
+        lo = np.where(up, mid, lo)
+        hi = np.where(up, hi, mid)
+    c = hi if as_double else hi.astype(F32)
+    x = (c.astype(np.float64) / c.astype(np.float64).sum()) * 65535.0
+    frac_dist = np.abs(x - np.round(x))
+    flag |= (frac_dist <= ulps * np.spacing(x.astype(F32)).astype(np.float64)) & (x > 0)
+    return flag
+
+
 def quantise(C_raw: np.ndarray, as_double: bool) -> np.ndarray:
     """(C / C.sum() * 65535).int() / 65535 (yumas.py:211; :97 in fp64)."""
     if as_double:

@@ -1,0 +1,162 @@
+"""BASELINE.json configs c3 and c4 on the HIP engine, and generic-float
+inputs with the summation-order tie window reported (SURVEY §7 hard parts).
+
+c3: a batched sweep of Yuma 4 scenarios drawn from bench.sweep_config's
+    bond_alpha x kappa x liquid x (alpha_low, alpha_high) grid at 256 x 4096,
+    every scenario against the oracle's run_simulation loop.
+c4: the wide subnet 256 x 65536 cut into 8 miner-column shards
+    (wide.run_wide_local) against the unsharded engine run and the oracle.
+Reference semantics: yumas.py:494-606 (Yuma4), :399-491 (Yuma3),
+simulation_utils.py:26-112 (epoch loop)."""
+
+from __future__ import annotations
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import assert_close
+from oracle import yuma_oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+from yuma_simulation._internal import engine, synth, wide  # noqa: E402
+from yuma_simulation._internal.yumas import YumaConfig, YumaParams  # noqa: E402
+
+import bench  # noqa: E402  (the c3 grid: bench.sweep_config)
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    assert torch.cuda.is_available(), "gpu tests need a ROCm GPU"
+    engine.load_library()
+    yield
+
+
+def _sweep_ids(n: int) -> list[int]:
+    rng = np.random.default_rng(0xC3)
+    ids = sorted(int(g) for g in rng.choice(4096, n, replace=False))
+    cfgs = [bench.sweep_config(g) for g in ids]
+    # both halves of the grid's liquid axis, several kappas and alphas
+    assert {c.liquid_alpha for c in cfgs} == {False, True}
+    assert len({c.kappa for c in cfgs}) >= 8 and len({c.bond_alpha for c in cfgs}) >= 8
+    return ids
+
+
+def test_c3_sweep_batch_matches_oracle():
+    """16 sweep scenarios x 8 epochs at 256 x 4096 in ONE batched engine call
+    (bench --config c3's launch), each against the oracle: C exact, the rest
+    within 1e-5 (north_star tolerance)."""
+    E, N, V, M = 8, 16, 256, 4096
+    version = "Yuma 4 (Rhef+relative bonds)"
+    ids = _sweep_ids(N)
+    cfgs = [bench.sweep_config(g) for g in ids]
+    params = [engine.make_params(engine.VARIANT_YUMA4, c) for c in cfgs]
+    seed = 0x5EED0003
+    W = engine.synth_weights(seed, E, N, V, M)
+    S = torch.from_numpy(synth.stakes(seed, E, N, V)).to(W.device)
+    res = engine.run(engine.VARIANT_YUMA4, params, W, S, want_hist=True)
+    C, Dn, I = res.C.cpu().numpy(), res.Dn.cpu().numpy(), res.I.cpu().numpy()
+    Bh = res.B_hist.cpu().numpy()
+    Wh, Sh = W.cpu().numpy(), S.cpu().numpy()
+    for j, (g, cfg) in enumerate(zip(ids, cfgs)):
+        ref = orc.run(version, Wh[:, j], Sh[:, j], cfg)
+        tag = f"sweep[{g}] ba={cfg.bond_alpha:.3f} k={cfg.kappa:.3f} liquid={cfg.liquid_alpha}"
+        np.testing.assert_array_equal(C[:, j], ref["C"], err_msg=tag)
+        assert_close(Dn[:, j], ref["Dn"], what=f"{tag} Dn")
+        assert_close(I[:, j], ref["I"], what=f"{tag} I")
+        assert_close(Bh[:, j], ref["B"], what=f"{tag} B")
+
+
+def test_c4_wide_eight_shards_matches_unsharded_and_oracle():
+    """256 x 65536 (1024 tiles of 64 miners) cut into 8 shards: C and the bond
+    history bit-equal to the unsharded engine run for 3 epochs; C, Dn and B
+    against the oracle for the first 2."""
+    E, V, M = 3, 256, 65536
+    cfg = YumaConfig()
+    params = [engine.make_params(engine.VARIANT_YUMA3, cfg)]
+    seed = 0x5EED0004
+    W = engine.synth_weights(seed, E, 1, V, M)
+    S = torch.from_numpy(synth.stakes(seed, E, 1, V)).to(W.device)
+    ref = engine.run(engine.VARIANT_YUMA3, params, W, S, want_hist=True)
+    got = wide.run_wide_local(engine.VARIANT_YUMA3, params, W, S, 8, want_hist=True)
+    torch.cuda.synchronize()
+    assert len(got.C) == 8
+    C = torch.cat(got.C, dim=2)
+    np.testing.assert_array_equal(C.cpu().numpy(), ref.C.cpu().numpy())
+    Bh = torch.cat(got.B_hist, dim=3)
+    assert torch.equal(Bh, ref.B_hist)
+    assert torch.equal(torch.cat(got.B_final, dim=2), ref.B_final)
+    assert_close(got.Dn.cpu().numpy(), ref.Dn.cpu().numpy(), what="Dn sharded vs unsharded")
+    assert_close(torch.cat(got.I, dim=2).cpu().numpy(), ref.I.cpu().numpy(), what="I sharded vs unsharded")
+    del ref
+    o = orc.run("Yuma 3 (Rhef)", W[:2, 0].cpu().numpy(), S[:2, 0].cpu().numpy(), cfg)
+    np.testing.assert_array_equal(C[:2, 0].cpu().numpy(), o["C"])
+    assert_close(got.Dn[:2, 0].cpu().numpy(), o["Dn"], what="Dn vs oracle")
+    assert_close(Bh[:2, 0].cpu().numpy(), o["B"], what="B vs oracle")
+
+
+def _tie_report(C_gpu, C_ref, W, S, cfg, as_double=False):
+    """(mismatched columns outside the tie window, tie-window size, mismatches inside)."""
+    flags = orc.tie_columns(W, S, cfg.kappa, cfg.consensus_precision, as_double)
+    bad = C_gpu != C_ref
+    return int((bad & ~flags).sum()), int(flags.sum()), int((bad & flags).sum())
+
+
+@pytest.mark.parametrize("variant,version", [(engine.VARIANT_YUMA3, "Yuma 3 (Rhef)"),
+                                             (engine.VARIANT_RUST, "Yuma 0 (subtensor)")])
+def test_random_float_epochs_tie_window(variant, version, record_property):
+    """8 epochs of uniform-random fp32 weights at 256 x 4096. Summation order
+    (torch's, numpy's, the engine's DPP trees) can only move consensus on
+    columns inside the tie window (oracle.tie_columns); everywhere else C is
+    bit-equal to the oracle, and while no column has moved, Dn / I / B are
+    within 1e-5. The window size and the in-window flips are reported."""
+    E, V, M = 8, 256, 4096
+    rng = np.random.default_rng(0x7E5 + variant)
+    W = rng.random((E, 1, V, M), dtype=np.float32)
+    W *= rng.random((E, 1, V, M), dtype=np.float32) < 0.5  # sparse rows, as real subnets
+    S = rng.random((E, 1, V), dtype=np.float32)
+    cfg = YumaConfig()
+    res = engine.run(variant, [engine.make_params(variant, cfg)], torch.from_numpy(W), torch.from_numpy(S),
+                     want_hist=True)
+    ref = orc.run(version, W[:, 0], S[:, 0], cfg)
+    C = res.C[:, 0].cpu().numpy()
+    total_win = total_flip = 0
+    for e in range(E):
+        outside, win, inside = _tie_report(C[e], ref["C"][e], W[e, 0], S[e, 0], cfg, variant == engine.VARIANT_RUST)
+        assert outside == 0, f"epoch {e}: {outside} columns differ outside the tie window"
+        total_win += win
+        total_flip += inside
+    record_property("tie_window_columns", total_win)
+    record_property("tie_window_flips", total_flip)
+    print(f"\n{version}: tie window {total_win} of {E * M} columns, {total_flip} flipped")
+    if total_flip == 0:
+        assert_close(res.Dn[:, 0].cpu().numpy(), ref["Dn"], what="Dn")
+        assert_close(res.I[:, 0].cpu().numpy(), ref["I"], what="I")
+        assert_close(res.B_hist[:, 0].cpu().numpy(), ref["B"], what="B")
+
+
+def test_wide_float_weights_against_oracle():
+    """miner-column shards on generic float weights. The shards'
+    row-sum partials add up in shard order, not the unsharded chunk order, so
+    bit-equality with the unsharded run is not claimed; against the oracle C
+    is exact outside the tie window and the rest within 1e-5."""
+    E, V, M = 4, 64, 1000
+    rng = np.random.default_rng(0x51DE)
+    W = rng.random((E, 1, V, M), dtype=np.float32)
+    S = rng.random((E, 1, V), dtype=np.float32)
+    cfg = YumaConfig(yuma_params=YumaParams(liquid_alpha=True))
+    params = [engine.make_params(engine.VARIANT_YUMA4, cfg)]
+    got = wide.run_wide_local(engine.VARIANT_YUMA4, params, torch.from_numpy(W), torch.from_numpy(S), 3,
+                              want_hist=True)
+    torch.cuda.synchronize()
+    ref = orc.run("Yuma 4 (Rhef+relative bonds) - liquid alpha on", W[:, 0], S[:, 0], cfg)
+    C = torch.cat(got.C, dim=2)[:, 0].cpu().numpy()
+    flips = 0
+    for e in range(E):
+        outside, _, inside = _tie_report(C[e], ref["C"][e], W[e, 0], S[e, 0], cfg)
+        assert outside == 0, f"epoch {e}"
+        flips += inside
+    if flips == 0:
+        assert_close(got.Dn[:, 0].cpu().numpy(), ref["Dn"], what="Dn")
+        assert_close(torch.cat(got.B_hist, dim=3)[:, 0].cpu().numpy(), ref["B"], what="B")

@@ -166,3 +166,17 @@ def test_oracle_large_random_floats(golden):
     np.testing.assert_array_equal(r["server_consensus_weight"], g["rand__server_consensus_weight"])
     assert_close(r["server_incentive"], g["rand__server_incentive"])
     assert_close(r["validator_reward_normalized"], g["rand__validator_reward_normalized"])
+
+
+def test_tie_columns_flags_exact_ties_only():
+    """oracle.tie_columns (the summation-order tie window of yumas.py:203-204,
+    :186, :211): a column whose stake sum above the bisection midpoint equals
+    kappa exactly is flagged; on random inputs few columns are."""
+    S = np.full(4, 0.25, np.float32)
+    W = np.array([[2, 1, 0], [2, 1, 0], [0, 1, 2], [0, 1, 2]], np.float32)
+    flags = orc.tie_columns(W, S, 0.5, 2**17)
+    assert flags[0] and flags[2]  # stake 0.5 above every mid below 2/3: == kappa
+    rng = np.random.default_rng(5)
+    Wr = rng.random((16, 64), dtype=np.float32)
+    Sr = rng.random(16, dtype=np.float32)
+    assert 0 < (~orc.tie_columns(Wr, Sr, 0.5, 2**17)).sum() and orc.tie_columns(Wr, Sr, 0.5, 2**17).mean() < 0.2

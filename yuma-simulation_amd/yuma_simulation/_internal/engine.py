@@ -344,9 +344,12 @@ def run(variant: int, params: list[YumaParamsC], W: torch.Tensor, S: torch.Tenso
         B_init: torch.Tensor | None = None, Wprev_init: torch.Tensor | None = None, *,
         want_hist: bool = False, want: tuple[str, ...] = (), chunk_epochs: int = 0,
         workspace: torch.Tensor | None = None, out: dict | None = None,
-        phase_ms: list | None = None, capture: list | None = None) -> RunResult:
+        phase_ms: list | None = None, capture: list | None = None,
+        single_call: bool = False) -> RunResult:
     """E epochs of N scenarios. W [E,N,V,M], S [E,N,V] (raw); optional
-    B_init [N,V,M] and (Yuma2) normalised Wprev_init [N,V,M]."""
+    B_init [N,V,M] and (Yuma2) normalised Wprev_init [N,V,M].
+    single_call: E == 1 through yuma_epoch (one call of a Yuma* variant,
+    yumas.py:61/175/285/399/494) instead of yuma_run."""
     dev = device()
     lib = load_library()
     E, N, V, M = W.shape
@@ -389,7 +392,13 @@ def run(variant: int, params: list[YumaParamsC], W: torch.Tensor, S: torch.Tenso
     args = (variant, prm.data_ptr(), N, E, V, M, W.data_ptr(), S.data_ptr(),
             _ptr(B_init), _ptr(Wprev_init), ctypes.addressof(outs),
             workspace.data_ptr(), workspace.numel(), int(chunk_epochs), stream)
-    if capture is not None:  # RunGraph: capture instead of launching
+    if single_call:  # one Yuma* call per slice: the yuma_epoch entry point
+        if E != 1 or capture is not None or phase_ms is not None:
+            raise ValueError("single_call is one epoch, launched directly")
+        _check(lib.yuma_epoch(variant, prm.data_ptr(), N, V, M, W.data_ptr(), _ptr(Wprev_init),
+                              S.data_ptr(), _ptr(B_init), ctypes.addressof(outs), workspace.data_ptr(),
+                              workspace.numel(), stream), "yuma_epoch")
+    elif capture is not None:  # RunGraph: capture instead of launching
         h = ctypes.c_void_p()
         torch.cuda.synchronize(dev)
         _check(lib.yuma_graph_create(ctypes.byref(h), *args[:-1]), "yuma_graph_create")

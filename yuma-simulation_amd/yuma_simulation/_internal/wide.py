@@ -17,8 +17,19 @@ depend on timing. Four small exchanges per run, independent of E:
 scenario uses liquid alpha), [E,N,V] dividend partials.
 
 The same orchestration drives several shards inside ONE process
-(`run_wide_local`), which the GPU tests use to check sharded == unsharded on
-one device; `run_wide_distributed` is the one-shard-per-rank form.
+(`run_wide_local`); `run_wide_distributed` is the one-shard-per-rank form.
+
+Exactness. Every rank gets the same bits for any shard count's totals, but
+those totals are added in shard order: ((shard0 + shard1) + shard2) ...,
+where the unsharded engine adds the same 256-miner chunk sums strictly left
+to right. The two orders give identical fp32 results whenever the partial
+sums are exact -- the integer-valued synthetic weights of the benchmarks,
+whose row sums stay below 2^24, are -- and that case is tested bit-for-bit
+against the unsharded run (tests/test_wide.py, test_gpu_configs.py c4). On
+generic float weights a row sum can differ by an ulp, which can move a
+consensus decision inside the tie window (oracle.tie_columns); that case is
+tested against the oracle: C exact outside the window, the rest within 1e-5
+(test_gpu_configs.test_wide_float_weights_against_oracle).
 """
 
 from __future__ import annotations

@@ -3,9 +3,9 @@
 Drop-in for src/yuma_simulation/_internal/yumas.py: same config dataclasses
 (with the same defaults and the same attribute flattening), same variant names,
 same function signatures and the same result dictionaries (keys, dtypes,
-Python-float vs tensor types). Every variant is one ``yuma_epoch``-equivalent
-engine launch sequence on the GPU (engine.run with E = 1 and every output
-requested); nothing is computed on the CPU. Results come back on the device
+Python-float vs tensor types). Every variant is one ``yuma_epoch`` C-ABI
+call on the GPU (engine.run(single_call=True), every output requested);
+nothing is computed on the CPU. Results come back on the device
 of the input ``W`` (CPU in, CPU out — as the reference returns them).
 """
 
@@ -120,7 +120,7 @@ def _epoch(variant: int, W: torch.Tensor, S: torch.Tensor, B_old, config: YumaCo
         variant, [prm], W.reshape(1, 1, V, M), S.reshape(1, 1, V),
         None if B_old is None else B_old.reshape(1, V, M),
         None if W_prev is None else W_prev.reshape(1, V, M),
-        want=tuple(want), chunk_epochs=1,
+        want=tuple(want), single_call=True,
     )
     x = res.extra
 
