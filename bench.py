@@ -19,9 +19,23 @@ Other BASELINE.json configs (`--config`, not what the driver runs):
   c5  the full dividend sheet (4 bond penalties x 14 cases x 9 versions =
       504 runs) through generate_total_dividends_tables.
 
-Prints ONE JSON line (rank 0) with the driver's fields plus `roofline`
-(dominant kernel, algorithmic bytes / measured device time from HIP events)
-and `cpu_baseline` (the numpy oracle on a bounded sample, host cores).
+Prints ONE JSON line (rank 0) with the driver's fields plus
+  roofline      SURVEY §8d step roofline: achieved = scenario-epochs/s per GPU x
+                BYTES(V,M) (the fp32 epoch-step contract, 12,617,728 B at
+                256 x 4096), frac = achieved / 8 TB/s; traffic = the rocprofv3
+                FETCH_SIZE + WRITE_SIZE bytes of one step (committed PMC passes of
+                this exact workload, profiles/r02/pmc_traffic.json), and
+                roofline.kernel = the dominant kernel (k_bonds_elem at c2):
+                algorithmic bytes per launch / its HIP-event launch time;
+  cpu_baseline  the torch-CPU restatement of the epoch (oracle/torch_cpu.py,
+                bit-identical to the reference goldens) on the host cores of
+                this box: vectorised (value) and reference-structured (per-column
+                Python bisection, as yumas.py runs it);
+  also          (default c2 run) the same line's numbers for "Yuma 4 liquid",
+                the second c2 version of SURVEY §7, on the same resident inputs.
+
+`--gpus N` without torchrun re-launches itself under torch.distributed.run
+with N local ranks (before anything touches a GPU).
 """
 
 from __future__ import annotations
@@ -74,42 +88,90 @@ def contract_bytes(V: int, M: int, variant: int) -> float:
     return float(b + (4 * V * M if variant == 2 else 0))
 
 
-def cpu_baseline(version: str, V: int, M: int, epochs: int, ring: int, seed: int) -> dict:
-    """The numpy oracle (oracle/yuma_oracle.py, a port of the reference
-    algorithm) on `epochs` epochs of the same workload, one host core."""
-    from oracle import yuma_oracle as orc
-    from yuma_simulation._internal import synth
-    from yuma_simulation._internal.yumas import YumaConfig
+def host_cpu() -> dict:
+    """The host this runs on: lscpu model, os.cpu_count(), the CPUs this
+    process may use, and the torch thread count the CPU baseline uses
+    (the process's CPU share, capped by OMP_NUM_THREADS when the scheduler
+    sets it: a 1-GPU box exposes the whole machine's CPUs to os.cpu_count()
+    but grants each GPU a share)."""
+    import subprocess
 
-    Wr = synth.weights(seed, ring, 1, V, M)[:, 0]
-    S = synth.stakes(seed, epochs, 1, V)[:, 0]
-    W = np.stack([Wr[e % ring] for e in range(epochs)])
-    t0 = time.perf_counter()
-    orc.run(version, W, S, YumaConfig())
-    dt = time.perf_counter() - t0
+    model = None
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            if line.startswith("Model name:"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except (OSError, subprocess.SubprocessError):
+        pass
+    if model is None and os.path.exists("/proc/cpuinfo"):
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    total = os.cpu_count() or 1
+    usable = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else total
+    threads = usable
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        threads = min(threads, int(omp))
+    return {"model": model, "cpu_count": total, "usable": usable, "threads": threads}
+
+
+def cpu_baseline(variant: str, W_dev, S_dev, cfgs: list, seconds: float, warmup: int, structured_epochs: int,
+                 label: str, ring: int = 64) -> dict:
+    """SURVEY §8d CPU baseline: oracle/torch_cpu.py (the epoch restated in torch
+    CPU ops, bit-identical to the reference goldens) on the host cores, over
+    the SAME resident inputs (the first `ring` epochs copied back from HBM and
+    cycled). value = the vectorised form (all columns' bisections per
+    iteration, torch intra-op threads), timed for about `seconds`;
+    `structured` = the reference's own loop structure (one Python bisection
+    per miner column, yumas.py:197-209), `structured_epochs` epochs."""
+    from oracle import torch_cpu as tc
+
+    host = host_cpu()
+    torch.set_num_threads(host["threads"])
+    n_sc = len(cfgs)
+    ring = min(ring, W_dev.shape[0])
+    W = W_dev[:ring, :n_sc].cpu()
+    S = S_dev[:ring, :n_sc].cpu()
+
+    def rate(mode: str, n_warm: int, max_epochs: int, budget: float) -> tuple[float, int, float]:
+        B = [None] * n_sc
+        for t in range(n_warm):
+            for j, cfg in enumerate(cfgs):
+                B[j] = tc.epoch(variant, W[t % ring, j], S[t % ring, j], B[j], cfg, consensus=mode)["validator_bonds"]
+        t0 = time.perf_counter()
+        n = 0
+        while n < max_epochs and (n == 0 or time.perf_counter() - t0 < budget):
+            t = n_warm + n
+            for j, cfg in enumerate(cfgs):
+                B[j] = tc.epoch(variant, W[t % ring, j], S[t % ring, j], B[j], cfg, consensus=mode)["validator_bonds"]
+            n += 1
+        dt = time.perf_counter() - t0
+        return n * n_sc / dt, n, dt
+
+    vec, vn, vdt = rate("vectorised", warmup, 100000, seconds)
+    st = None
+    if structured_epochs > 0:
+        st = rate("structured", 1, structured_epochs, float("inf"))
     return {
-        "value": round(epochs / dt, 3),
+        "value": round(vec, 3),
         "unit": "scenario-epochs/s",
-        "cores": 1,
+        "cores": host["threads"],
         "kind": "port",
-        "sample": f"{epochs} epochs of {version} at {V}x{M} ({ring} distinct synthetic W epochs cycled), "
-                  f"vectorised numpy oracle, 1 thread, {dt:.1f} s",
+        "sample": (f"{label}: oracle/torch_cpu.py vectorised, {warmup} warm-up + {vn} timed epochs x {n_sc} "
+                   f"scenario(s) cycling the first {ring} resident epochs ({vdt:.1f} s), torch {host['threads']} "
+                   f"threads on {host['model']} (os.cpu_count() = {host['cpu_count']}, {host['usable']} usable); "
+                   f"bit-identical to the reference goldens (tests/test_oracle_golden.py)"),
+        "structured": None if st is None else {
+            "value": round(st[0], 4), "unit": "scenario-epochs/s", "cores": 1,
+            "sample": f"reference-structured per-column Python bisection, 1 warm-up + {st[1]} timed epochs x "
+                      f"{n_sc} scenario(s) ({st[2]:.1f} s)"},
+        "host": host,
     }
-
-
-def load_traffic(cfg: dict, dominant: str):
-    """HBM bytes per launch from committed rocprofv3 PMC passes
-    (profiles/pmc_traffic.json, written by tools/pmc_traffic.py), if they were
-    collected on this exact workload."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if not os.path.exists(path):
-        return None
-    with open(path) as f:
-        rec = json.load(f)
-    if rec.get("workload") != cfg:
-        return None
-    k = rec.get("kernels", {}).get(dominant)
-    return None if k is None else k.get("hbm_bytes_per_scenario_epoch")
 
 
 def timed(step, warmup: int, steps: int, dist: bool, dev) -> float:
@@ -172,6 +234,94 @@ def sweep_config(g: int):
                                              alpha_low=lo, alpha_high=hi))
 
 
+def engine_line(args, variant: int, params: list, W, S, world: int, dist: bool, workload: dict) -> dict:
+    """Time one engine configuration on resident inputs and build its line:
+    the step (graph replay of the whole E-epoch run), per-phase HIP-event
+    device time, the §8d step roofline and the dominant kernel's roofline."""
+    from yuma_simulation._internal import engine
+
+    dev = W.device
+    E, N, V, M = W.shape
+    liquid = any(p.liquid_mode != engine.LIQUID_OFF for p in params)
+    hist = not args.no_history
+    out = {"Dn": torch.empty(E, N, V, device=dev), "C": torch.empty(E, N, M, device=dev),
+           "I": torch.empty(E, N, M, device=dev), "B_final": torch.empty(N, V, M, device=dev)}
+    if hist:
+        out["B_hist"] = torch.empty(E, N, V, M, device=dev)
+    ws = torch.empty(engine.workspace_bytes(variant, N, E, V, M, False), dtype=torch.uint8, device=dev)
+    chunk = args.chunk
+    graph = None
+    if args.no_graph:
+        def step():
+            return engine.run(variant, params, W, S, want_hist=hist, out=out, workspace=ws, chunk_epochs=chunk)
+    else:
+        # the whole E-epoch run captured once into a HIP graph (yuma_graph_create);
+        # each timed step is one replay of it over the same resident inputs
+        graph = engine.RunGraph(variant, params, W, S, want_hist=hist, out=out, workspace=ws, chunk_epochs=chunk)
+        step = graph.launch
+
+    elapsed = timed(step, args.warmup, args.steps, dist, dev)
+    units = E * N  # scenario-epochs per step per GPU
+    value = float(units) * world * args.steps / elapsed
+
+    # per-phase device time from HIP events recorded on the launch stream
+    # (yuma_run_profiled: separate, untimed runs of the same step)
+    phases = np.zeros(len(engine.PHASES))
+    for _ in range(args.profile_reps):
+        buf = [0.0] * len(engine.PHASES)
+        engine.run(variant, params, W, S, want_hist=hist, out=out, workspace=ws, chunk_epochs=chunk, phase_ms=buf)
+        phases += np.array(buf)
+    phases /= args.profile_reps
+    if graph is not None:
+        graph.close()
+    eff_chunk = chunk if 0 < chunk <= E else E
+    launches = -(-E // eff_chunk)  # launches of each phase kernel per step
+    phase_info = {}
+    for i, name in enumerate(engine.PHASES):
+        if phases[i] <= 0:
+            continue
+        b = phase_bytes(name, V, M, variant, liquid, hist, eff_chunk) * units
+        phase_info[name] = {"kernel": kernel_of(name, variant), "ms": round(float(phases[i]), 4),
+                            "GBps": round(b / (phases[i] * 1e-3) / 1e9, 1)}
+    dom = int(np.argmax(phases))
+    dom_name = engine.PHASES[dom]
+    dom_kernel = kernel_of(dom_name, variant)
+    dom_bytes = phase_bytes(dom_name, V, M, variant, liquid, hist, eff_chunk) * units / launches
+    dom_ms = float(phases[dom]) / launches
+    k_achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
+
+    contract = contract_bytes(V, M, variant)
+    per_gpu = value / world
+    achieved = per_gpu * contract / 1e9
+    key = {k: workload[k] for k in ("V", "M", "epochs", "scenarios_per_gpu", "version", "bond_history")}
+    pmc = load_traffic(key)
+    line = base_line(args, world, value, "scenario-epochs/s", elapsed, "weak", workload)
+    line["roofline"] = {
+        "bound": "hbm",
+        "achieved": round(achieved, 1),
+        "peak": HBM_PEAK_GBPS,
+        "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBPS, 4),
+        "traffic": None if pmc is None else round(sum(pmc.values()) * units),
+        "definition": (f"SURVEY 8d step roofline: scenario-epochs/s per GPU x BYTES(V,M) = {contract:,.0f} B "
+                       "(read W, B, S; write B, Dn, C, I) / 8 TB/s; traffic = rocprofv3 FETCH_SIZE + WRITE_SIZE "
+                       "bytes of one step (profiles/r02/pmc_traffic.json)"),
+        "contract_bytes_per_step": contract * units,
+        "kernel": {
+            "name": dom_kernel,
+            "launches_per_step": launches,
+            "avg_ms": round(dom_ms, 4),
+            "bytes_per_launch": dom_bytes,
+            "achieved": round(k_achieved, 1),
+            "frac": round(k_achieved / HBM_PEAK_GBPS, 4),
+            "traffic": None if pmc is None or dom_kernel not in pmc else round(pmc[dom_kernel] * units / launches),
+            "timing": "HIP events on the launch stream around the kernel (yuma_run_profiled)",
+        },
+    }
+    line["phases"] = phase_info
+    return line
+
+
 def bench_engine(args, world: int, rank: int, dist: bool) -> dict:
     """c2 (default) and c3: engine.run over E epochs of N scenarios per GPU."""
     from yuma_simulation._internal import engine, synth
@@ -181,10 +331,11 @@ def bench_engine(args, world: int, rank: int, dist: bool) -> dict:
     dev = engine.device()
     E, V, M, N = args.epochs, args.validators, args.miners, args.scenarios
     variant, _ = resolve_version(args.version)
+    liquid_version = args.version.endswith("liquid alpha on")
     if args.config == "c3":
         cfgs = [sweep_config(rank * N + i) for i in range(N)]
     else:
-        cfgs = [YumaConfig(yuma_params=YumaParams(liquid_alpha=args.liquid))] * N
+        cfgs = [YumaConfig(yuma_params=YumaParams(liquid_alpha=args.liquid or liquid_version))] * N
     params = [engine.make_params(variant, c) for c in cfgs]
     liquid = any(p.liquid_mode != engine.LIQUID_OFF for p in params)
     hist = not args.no_history
@@ -193,90 +344,34 @@ def bench_engine(args, world: int, rank: int, dist: bool) -> dict:
     # inputs resident in HBM before timing
     W = engine.synth_weights(seed, E, N, V, M)
     S = torch.from_numpy(synth.stakes(seed, E, N, V)).to(dev)
-    out = {"Dn": torch.empty(E, N, V, device=dev), "C": torch.empty(E, N, M, device=dev),
-           "I": torch.empty(E, N, M, device=dev), "B_final": torch.empty(N, V, M, device=dev)}
-    if hist:
-        out["B_hist"] = torch.empty(E, N, V, M, device=dev)
-    ws = torch.empty(engine.workspace_bytes(variant, N, E, V, M, False), dtype=torch.uint8, device=dev)
-    chunk = args.chunk
 
-    if args.no_graph:
-        def step():
-            return engine.run(variant, params, W, S, want_hist=hist, out=out, workspace=ws, chunk_epochs=chunk)
-    else:
-        # the whole E-epoch run captured once into a HIP graph (yuma_graph_create);
-        # each timed step is one replay of it over the same resident inputs
-        graph = engine.RunGraph(variant, params, W, S, want_hist=hist, out=out, workspace=ws,
-                                chunk_epochs=chunk)
-        step = graph.launch
-
-    elapsed = timed(step, args.warmup, args.steps, dist, dev)
-    value = float(E) * N * world * args.steps / elapsed
-
-    # per-phase device time from HIP events on the launch stream (separate,
-    # untimed passes of the same step)
-    phases = np.zeros(len(engine.PHASES))
-    for _ in range(args.profile_reps):
-        buf = [0.0] * len(engine.PHASES)
-        engine.run(variant, params, W, S, want_hist=hist, out=out, workspace=ws, chunk_epochs=chunk,
-                   phase_ms=buf)
-        phases += np.array(buf)
-    phases /= args.profile_reps
-    eff_chunk = chunk if 0 < chunk <= E else E
-    units = E * N
-    phase_info = {}
-    for i, name in enumerate(engine.PHASES):
-        b = phase_bytes(name, V, M, variant, liquid, hist, eff_chunk) * units
-        phase_info[name] = {"ms": round(float(phases[i]), 4),
-                            "GBps": round(b / (phases[i] * 1e-3) / 1e9, 1) if phases[i] > 0 else None}
-    dom = int(np.argmax(phases))
-    dom_name = engine.PHASES[dom]
-    dom_bytes = phase_bytes(dom_name, V, M, variant, liquid, hist, eff_chunk) * units
-    achieved = dom_bytes / (phases[dom] * 1e-3) / 1e9
-    if args.config == "c3":
-        wl = (f"c3: parameter sweep, {N} scenarios per GPU (of the 4096-point bond_alpha x kappa x "
-              f"liquid x alpha grid) of {V}V x {M}M x {E} epochs, {args.version}")
-    else:
-        wl = f"c2: single subnet {V}V x {M}M x {E} epochs, {args.version}" + (" liquid" if liquid else "")
-    workload = {"workload": wl, "V": V, "M": M, "epochs": E, "scenarios_per_gpu": N, "version": args.version,
+    def workload_of(version: str, liq: bool) -> dict:
+        if args.config == "c3":
+            wl = (f"c3: parameter sweep, {N} scenarios per GPU (of the 4096-point bond_alpha x kappa x "
+                  f"liquid x alpha grid) of {V}V x {M}M x {E} epochs, {version}")
+        else:
+            wl = f"c2: single subnet {V}V x {M}M x {E} epochs, {version}" + (" (liquid)" if liq else "")
+        return {"workload": wl, "V": V, "M": M, "epochs": E, "scenarios_per_gpu": N, "version": version,
                 "bond_history": hist, "launch": "direct" if args.no_graph else "hipGraph replay",
                 "parallelism": f"scenario-sharded x{world}" if world > 1 else "single GPU"}
-    traffic = load_traffic({k: workload[k] for k in ("V", "M", "epochs", "version", "bond_history")}, dom_name)
-    line = base_line(args, world, value, "scenario-epochs/s", elapsed, "weak", workload)
-    line["roofline"] = {
-        "bound": "hbm",
-        "kernel": f"k_{dom_name}",
-        "achieved": round(achieved, 1),
-        "peak": HBM_PEAK_GBPS,
-        "unit": "GB/s",
-        "frac": round(achieved / HBM_PEAK_GBPS, 4),
-        "traffic": traffic,
-    }
-    line["contract_GBps"] = round(value / world * contract_bytes(V, M, variant) / 1e9, 1)
-    line["phases"] = phase_info
+
+    line = engine_line(args, variant, params, W, S, world, dist, workload_of(args.version, liquid))
+    if args.config == "c2" and not args.no_also:
+        # SURVEY §7 "Config 2 naming": c2 is quoted for Yuma 3 AND Yuma 4 liquid
+        v4 = "Yuma 4 (Rhef+relative bonds) - liquid alpha on"
+        p4 = [engine.make_params(4, YumaConfig(yuma_params=YumaParams(liquid_alpha=True)))] * N
+        l4 = engine_line(args, 4, p4, W, S, world, dist, workload_of(v4, True))
+        line["also"] = {v4: {k: l4[k] for k in ("value", "unit", "ms_per_step", "roofline", "phases", "config")}}
     if rank == 0 and not args.no_cpu_baseline:
         if args.config == "c3":
-            line["cpu_baseline"] = cpu_baseline_c3(args.version, V, M, args.seed)
+            line["cpu_baseline"] = cpu_baseline("yuma4" if variant == 4 else "yuma3", W, S, cfgs[:8], 10.0, 1, 1,
+                                                "c3: first 8 sweep scenarios")
         else:
-            line["cpu_baseline"] = cpu_baseline(args.version, V, M, args.cpu_epochs, 16, args.seed)
+            vname = {3: "yuma3", 4: "yuma4"}.get(variant)
+            if vname is not None:
+                line["cpu_baseline"] = cpu_baseline(vname, W, S, cfgs[:1], 10.0, 2, args.cpu_structured_epochs,
+                                                    f"c2: {args.version}")
     return line
-
-
-def cpu_baseline_c3(version: str, V: int, M: int, seed: int) -> dict:
-    """Oracle on 8 scenarios x 16 epochs of the c3 sweep (one host core)."""
-    from oracle import yuma_oracle as orc
-    from yuma_simulation._internal import synth
-
-    n_s, E = 8, 16
-    W = synth.weights(seed, E, n_s, V, M)
-    S = synth.stakes(seed, E, n_s, V)
-    t0 = time.perf_counter()
-    for i in range(n_s):
-        orc.run(version, W[:, i], S[:, i], sweep_config(i * 257))
-    dt = time.perf_counter() - t0
-    return {"value": round(n_s * E / dt, 3), "unit": "scenario-epochs/s", "cores": 1, "kind": "port",
-            "sample": f"{n_s} sweep scenarios x {E} epochs of {version} at {V}x{M}, numpy oracle, 1 thread, "
-                      f"{dt:.1f} s"}
 
 
 def bench_wide(args, world: int, rank: int, dist: bool) -> dict:
@@ -309,11 +404,18 @@ def bench_wide(args, world: int, rank: int, dist: bool) -> dict:
                 "version": args.version, "bond_history": hist,
                 "parallelism": f"miner-column sharded x{world} (all-gather of per-shard partials)"}
     line = base_line(args, world, value, "scenario-epochs/s", elapsed, "strong", workload)
-    line["roofline"] = {"bound": "hbm", "kernel": "whole epoch step (all stages; contract bytes / wall time)",
-                        "achieved": round(per_gpu_bytes, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                        "frac": round(per_gpu_bytes / HBM_PEAK_GBPS, 4), "traffic": None}
-    if rank == 0 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(args.version, V, M, 3, 3, args.seed)
+    pmc = load_traffic({k: workload[k] for k in ("V", "M", "epochs", "scenarios_per_gpu", "version",
+                                                  "bond_history")}) if world == 1 else None
+    line["roofline"] = {"bound": "hbm", "achieved": round(per_gpu_bytes, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                        "frac": round(per_gpu_bytes / HBM_PEAK_GBPS, 4),
+                        "traffic": None if pmc is None else round(sum(pmc.values()) * E),
+                        "definition": "SURVEY 8d step roofline per GPU: BYTES(V, M/world) x epochs/s / 8 TB/s "
+                                      "(all stages and exchanges inside the wall time)"}
+    if rank == 0 and not args.no_cpu_baseline and variant in (3, 4):
+        Wc = engine.synth_weights(args.seed, 3, 1, V, M)  # the full-width first epochs, for the CPU
+        line["cpu_baseline"] = cpu_baseline({3: "yuma3", 4: "yuma4"}[variant], Wc, S, [YumaConfig()], 10.0, 1, 0,
+                                            f"c4: {args.version} at {V}x{M}")
+        del Wc
     return line
 
 
@@ -364,8 +466,9 @@ def bench_sheet(args, world: int, rank: int, dist: bool) -> dict:
                     validators=r.case.validators)
         dt = time.perf_counter() - t0
         line["cpu_baseline"] = {"value": round(units / dt, 1), "unit": "scenario-epochs/s", "cores": 1,
-                                "kind": "port", "sample": f"all {len(runs)} sheet runs, numpy oracle, 1 thread, "
-                                                          f"{dt:.1f} s"}
+                                "kind": "port", "sample": f"all {len(runs)} sheet runs, numpy oracle "
+                                                          f"(oracle/yuma_oracle.py), 1 thread, {dt:.1f} s",
+                                "host": host_cpu()}
     return line
 
 
@@ -395,8 +498,10 @@ def main():
     ap.add_argument("--no-graph", action="store_true",
                     help="c2/c3: launch each step directly instead of replaying a captured hipGraph")
     ap.add_argument("--seed", type=lambda s: int(s, 0), default=None)
-    ap.add_argument("--cpu-epochs", type=int, default=400)
+    ap.add_argument("--cpu-structured-epochs", type=int, default=10,
+                    help="c2: timed epochs of the reference-structured CPU baseline (0 = skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-also", action="store_true", help="c2: skip the Yuma 4 liquid companion line")
     ap.add_argument("--profile-reps", type=int, default=3)
     args = ap.parse_args()
     E, V, M, N, version, hist = DEFAULTS[args.config]
@@ -410,7 +515,21 @@ def main():
     if args.seed is None:
         args.seed = {"c3": 0x5EED0003, "c4": 0x5EED0004}.get(args.config, 0x5EED0002)
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # one process per GPU: re-launch under torch.distributed.run before
+        # anything here has touched a GPU, and exit with its status
+        import socket
+        import subprocess
+
+        with socket.socket() as sk:
+            sk.bind(("127.0.0.1", 0))
+            port = sk.getsockname()[1]
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+               "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *sys.argv[1:]]
+        sys.exit(subprocess.call(cmd))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus and "WORLD_SIZE" in os.environ:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = world > 1

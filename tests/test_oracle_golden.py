@@ -180,3 +180,76 @@ def test_tie_columns_flags_exact_ties_only():
     Wr = rng.random((16, 64), dtype=np.float32)
     Sr = rng.random(16, dtype=np.float32)
     assert 0 < (~orc.tie_columns(Wr, Sr, 0.5, 2**17)).sum() and orc.tie_columns(Wr, Sr, 0.5, 2**17).mean() < 0.2
+
+
+# ---------------------------------------------------------------------------
+# oracle/torch_cpu.py: the CPU baseline's restatement, bit-for-bit
+# ---------------------------------------------------------------------------
+def _torch_cases():
+    for iname in ("synth16x64", "rand16x64", "edge3x5"):
+        for variant in ("yuma3", "yuma4"):
+            for cname in specs.CONFIGS:
+                if cname.startswith("liquid") and variant == "yuma3":
+                    continue
+                yield iname, variant, cname
+
+
+def _bits_equal(a, e, what):
+    a = np.asarray(a, np.float32)
+    e = np.asarray(e, np.float32)
+    assert a.shape == e.shape, what
+    assert np.array_equal(a.view(np.uint32), e.view(np.uint32)) or np.array_equal(a, e, equal_nan=True), what
+
+
+@pytest.mark.parametrize("iname,variant,cname", list(_torch_cases()))
+def test_torch_cpu_structured_bit_identical_small(golden, iname, variant, cname):
+    """The reference-structured torch restatement (SURVEY §8d baseline (i))
+    reproduces the reference's full result dicts bit for bit."""
+    import torch
+
+    from oracle import torch_cpu as tc
+
+    g = golden("epoch_small.npz")
+    cfg = config_from(specs.CONFIGS[cname])
+    B = None
+    for step in ("e0", "e1"):
+        e = step[1]
+        W = torch.from_numpy(g[f"in__{iname}__W{e}"])
+        S = torch.from_numpy(g[f"in__{iname}__S{e}"])
+        for mode in ("structured", "vectorised"):
+            r = tc.epoch(variant, W, S, B, cfg, consensus=mode)
+            tag = f"out__{iname}__{variant}__{cname}__{step}"
+            keys = [k[len(tag) + 2:] for k in g.files if k.startswith(tag + "__") and not k.endswith("__pyfloat")]
+            assert set(keys) == set(r), tag
+            for k in keys:
+                _bits_equal(r[k].numpy(), g[f"{tag}__{k}"], f"{tag} {k} ({mode})")
+        B = r["validator_bonds"].clone()
+
+
+@pytest.mark.parametrize("name", ["yuma3", "yuma4", "yuma4_liquid"])
+def test_torch_cpu_bit_identical_large(large_inputs, name):
+    """256 x 4096 (the c2 shape), two epochs: consensus, rank, incentive,
+    prerank, dividends and the sampled bonds bit-identical to the reference
+    for both consensus forms (the benchmark's dyadic stakes make the
+    vectorised column sums order-independent)."""
+    import torch
+
+    from oracle import torch_cpu as tc
+
+    g, W, S = large_inputs
+    variant = name.split("_")[0]
+    cfg = config_from(specs.LARGE_SPECS[name])
+    idx = g["sample_idx"]
+    for mode in ("vectorised", "structured"):
+        B = None
+        for t, step in enumerate(("e0", "e1")):
+            r = tc.epoch(variant, torch.from_numpy(W[t]), torch.from_numpy(S[t]), B, cfg, consensus=mode)
+            B = r["validator_bonds"]
+            tag = f"out__{name}__{step}"
+            for k in ("server_consensus_weight", "server_incentive", "server_rank", "server_prerank",
+                      "validator_reward", "validator_reward_normalized"):
+                _bits_equal(r[k].numpy(), g[f"{tag}__{k}"], f"{tag} {k} ({mode})")
+            Bn = B.numpy()
+            _bits_equal(Bn[idx[:, 0], idx[:, 1]], g[f"{tag}__B_sample"], f"{tag} B_sample ({mode})")
+            assert_close(Bn.astype(np.float64).sum(axis=0), g[f"{tag}__B_colsum"], rtol=1e-12, atol_frac=0,
+                         what=f"{tag} B colsum ({mode})")

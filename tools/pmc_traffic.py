@@ -1,4 +1,5 @@
-"""Turn rocprofv3 PMC passes into per-kernel HBM bytes (profiles/pmc_traffic.json).
+"""Turn rocprofv3 PMC passes into per-kernel HBM bytes (profiles/r02/pmc_traffic.json,
+one record per bench workload; bench.py reads roofline.traffic from it).
 
 Two separate counter passes of the same bench command (MI355X_MICROARCH.md
 §HBM: FETCH_SIZE and WRITE_SIZE do not fit one pass):
@@ -23,24 +24,15 @@ import csv
 import glob
 import json
 import os
+import re
 import statistics
 from collections import defaultdict
 
-PHASE_OF = {  # kernel name fragment -> bench phase name
-    "k_rowsum": "rowsum",
-    "k_consensus": "consensus",
-    "k_quantise": "quantise",
-    "k_rank": "rank",
-    "k_incentive": "incentive",
-    "k_bonds": "bonds",
-    "k_finalize": "finalize",
-    "k_phase1": "phase1_fused",
-    "k_liquid": "liquid",
-}
+KERNEL_RE = re.compile(r"\b(k_[A-Za-z0-9_]+)")
 
 
 def counters(directory: str, name: str) -> dict[str, list[float]]:
-    """kernel phase -> list of per-dispatch counter values (KiB)."""
+    """kernel name -> list of per-dispatch counter values (KiB)."""
     files = glob.glob(os.path.join(directory, "**", "*counter_collection*.csv"), recursive=True)
     if not files:
         raise SystemExit(f"no counter_collection csv under {directory}")
@@ -56,10 +48,9 @@ def counters(directory: str, name: str) -> dict[str, list[float]]:
                 kname[key] = row.get("Kernel_Name", "")
     out: dict[str, list[float]] = defaultdict(list)
     for key, v in per_dispatch.items():
-        for frag, phase in PHASE_OF.items():
-            if frag in kname[key]:
-                out[phase].append(v)
-                break
+        m = KERNEL_RE.search(kname[key])
+        if m and m.group(1) != "k_synth":
+            out[m.group(1)].append(v)
     return out
 
 
@@ -73,34 +64,43 @@ def main():
     ap.add_argument("--M", type=int, default=4096)
     ap.add_argument("--version", default="Yuma 3 (Rhef)")
     ap.add_argument("--history", action="store_true")
-    ap.add_argument("--out", default=os.path.join(os.path.dirname(__file__), "..", "profiles", "pmc_traffic.json"))
+    ap.add_argument("--out", default=os.path.join(os.path.dirname(__file__), "..", "profiles", "r02",
+                                                  "pmc_traffic.json"))
+    ap.add_argument("--launches", type=int, default=1, help="launches of each kernel per bench step")
     a = ap.parse_args()
     fetch = counters(a.fetch_dir, "FETCH_SIZE")
     write = counters(a.write_dir, "WRITE_SIZE")
     units = a.epochs * a.scenarios
     kernels = {}
-    for phase in sorted(set(fetch) | set(write)):
-        f = statistics.median(fetch[phase]) if fetch.get(phase) else 0.0
-        w = statistics.median(write[phase]) if write.get(phase) else 0.0
+    for k in sorted(set(fetch) | set(write)):
+        f = statistics.median(fetch[k]) if fetch.get(k) else 0.0
+        w = statistics.median(write[k]) if write.get(k) else 0.0
         read_b = 2.0 * f * 1024.0   # gfx950: FETCH_SIZE = half of wide streaming reads
         write_b = w * 1024.0
-        kernels[phase] = {
+        kernels[k] = {
             "fetch_size_kib_raw": f,
             "write_size_kib": w,
             "hbm_read_bytes_per_launch": read_b,
             "hbm_write_bytes_per_launch": write_b,
             "hbm_bytes_per_launch": read_b + write_b,
-            "hbm_bytes_per_scenario_epoch": (read_b + write_b) / units,
-            "dispatches": [len(fetch.get(phase, [])), len(write.get(phase, []))],
+            "hbm_bytes_per_scenario_epoch": (read_b + write_b) * a.launches / units,
+            "dispatches": [len(fetch.get(k, [])), len(write.get(k, []))],
         }
     rec = {
-        "workload": {"V": a.V, "M": a.M, "epochs": a.epochs, "version": a.version,
-                     "bond_history": bool(a.history)},
+        "workload": {"V": a.V, "M": a.M, "epochs": a.epochs, "scenarios_per_gpu": a.scenarios,
+                     "version": a.version, "bond_history": bool(a.history)},
         "correction": "FETCH_SIZE x2 (gfx950 wide-read half count), KiB -> bytes; WRITE_SIZE as is",
+        "step_hbm_bytes": sum(v["hbm_bytes_per_launch"] for v in kernels.values()) * a.launches,
         "kernels": kernels,
     }
+    recs = []
+    if os.path.exists(a.out):
+        with open(a.out) as f:
+            recs = [r for r in json.load(f) if r.get("workload") != rec["workload"]]
+    recs.append(rec)
+    os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)
     with open(a.out, "w") as f:
-        json.dump(rec, f, indent=1)
+        json.dump(recs, f, indent=1)
     print(json.dumps(rec, indent=1))
 
 

@@ -2889,8 +2889,7 @@ void launch_rank(RowCfg rc, long long nblocks, hipStream_t st, const float* W, c
                  int V, int M, long long slice0, int tiles, float* R, float* rpart, float* Wn,
                  float* Wc, float* tvc, float* tvn) {
   const bool full = Wn != nullptr || Wc != nullptr || tvc != nullptr;
-  const char* rk = getenv("YUMA_RANK");  // YUMA_RANK=w: the register-resident kernel (A/B)
-  if (!full && !yuma2 && !(rk != nullptr && rk[0] == 'w')) {
+  if (!full && !yuma2) {  // streaming rank; k_rank_w also materialises Wn / Wc / T_v or clips W_prev
     YK_LAUNCH(yk::k_rank_s<VEC>, nblocks, 256, st, W, rsd, sn, C, N, V, M, slice0, tiles, R, rpart);
     return;
   }
