@@ -81,6 +81,38 @@ def phase_bytes(phase: str, V: int, M: int, variant: int, liquid: bool, hist: bo
     return float(table[phase])
 
 
+PHASE_KERNELS = {"rowsum": "k_rowsum", "consensus": "k_consensus_w", "quantise": "k_quantise",
+                 "rank": "k_rank_s", "incentive": "k_incentive", "finalize": "k_finalize",
+                 "fused1": "k_fused1", "liquid": "k_liquid"}
+
+
+def kernel_of(phase: str, variant: int) -> str:
+    """The kernel that runs a phase (as rocprofv3 names it) for run outputs:
+    the bond scan is k_bonds_elem for Yuma 3/4 and k_bonds (column-normalised
+    EMA) for YumaRust / Yuma 1 / Yuma 2."""
+    if phase == "bonds":
+        return "k_bonds_elem" if variant >= 3 else "k_bonds"
+    return PHASE_KERNELS[phase]
+
+
+TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r02", "pmc_traffic.json")
+
+
+def load_traffic(key: dict) -> dict | None:
+    """Per-kernel HBM bytes per scenario-epoch (FETCH_SIZE + WRITE_SIZE,
+    corrected) of the committed PMC passes of this exact workload, or None."""
+    try:
+        with open(TRAFFIC_JSON) as f:
+            records = json.load(f)
+    except (OSError, ValueError):
+        return None
+    for rec in records:
+        wl = rec.get("workload", {})
+        if all(wl.get(k) == v for k, v in key.items()):
+            return {k: float(v["hbm_bytes_per_scenario_epoch"]) for k, v in rec["kernels"].items()}
+    return None
+
+
 def contract_bytes(V: int, M: int, variant: int) -> float:
     """SURVEY §8d epoch-step contract: read W_t, B_{t-1}, S_t; write B_t, Dn_t,
     C_t, I_t (Yuma2 adds W_prev)."""

@@ -208,3 +208,23 @@ def test_scripts_import_without_gpu():
     sys.path.insert(0, root)
     for name in ("scripts.total_dividends_sheet_generator", "scripts.charts_table_generator"):
         assert callable(importlib.import_module(name).main)
+
+
+def test_bench_line_helpers():
+    """bench.py's phase -> kernel names and committed PMC traffic lookup (the
+    pieces of the JSON line that need no GPU)."""
+    import sys
+
+    sys.path.insert(0, ROOT)
+    import bench
+
+    for variant in range(5):
+        for phase in engine.PHASES:
+            assert bench.kernel_of(phase, variant).startswith("k_")
+    assert bench.kernel_of("bonds", engine.VARIANT_YUMA3) == "k_bonds_elem"
+    key = {"V": 256, "M": 4096, "epochs": 1000, "scenarios_per_gpu": 1, "version": "Yuma 3 (Rhef)",
+           "bond_history": True}
+    pmc = bench.load_traffic(key)
+    assert pmc is not None and pmc["k_bonds_elem"] > 8e6
+    assert bench.load_traffic(dict(key, M=1)) is None
+    assert bench.contract_bytes(256, 4096, 3) == 12_617_728
