@@ -73,17 +73,12 @@ def phase_bytes(phase: str, V: int, M: int, variant: int, liquid: bool, hist: bo
         "bonds": (4 * VM + 8 * V + 4 * M + (4 * M if colnorm else 0) + (4 * M if liquid else 0)
                   + (4 * VM if hist else 0) + 4 * V * tiles + 8 * VM / max(chunk, 1)),
         "finalize": 4 * V * tiles + 4 * V + 4 * V,
-        # one W read; writes rs, S/sum S, C_raw (f64), C, levels, R, tile sums
-        # one W read; S read; writes rs, S/sum S, C, levels, R, tile sums
-        "fused1": 4 * VM + 4 * V + 8 * V + 4 * M + 4 * M + 4 * M + 4 * ((M + 31) // 32),
-        "liquid": (4 * M + 4 * M + 4 * M) if liquid else 8 * M,
     }
     return float(table[phase])
 
 
 PHASE_KERNELS = {"rowsum": "k_rowsum", "consensus": "k_consensus_w", "quantise": "k_quantise",
-                 "rank": "k_rank_s", "incentive": "k_incentive", "finalize": "k_finalize",
-                 "fused1": "k_fused1", "liquid": "k_liquid"}
+                 "rank": "k_rank_s", "incentive": "k_incentive", "finalize": "k_finalize"}
 
 
 def kernel_of(phase: str, variant: int) -> str:

@@ -181,9 +181,7 @@ enum yuma_phase {
   YUMA_PHASE_INCENTIVE = 4, /* k_incentive: incentive, trust                    */
   YUMA_PHASE_BONDS = 5,     /* k_bonds:     bond recurrence over the chunk      */
   YUMA_PHASE_FINALIZE = 6,  /* k_finalize:  dividends                           */
-  YUMA_PHASE_FUSED1 = 7,    /* k_fused1:    phases 0,1,2(levels),3 in one W pass  */
-  YUMA_PHASE_LIQUID = 8,    /* k_liquid:    liquid-alpha quantiles (fused path)   */
-  YUMA_NUM_PHASES = 9
+  YUMA_NUM_PHASES = 7
 };
 
 /* yuma_run plus per-phase device time: HIP events are recorded on `stream`
@@ -261,23 +259,6 @@ int yuma_shard_stage(int stage, int variant, const yuma_params_t* params_dev, in
  * Bit-identical to yuma_simulation._internal.synth.weights (numpy).          */
 int yuma_synth_weights(uint64_t seed, int E, int N, int V, int M, int t0, float* W,
                        void* stream);
-
-/* Phase-1 path selection for this process (tests and A/B runs):
- * YUMA_PATH_AUTO (default) and YUMA_PATH_MULTIPASS run the multi-pass
- * kernels; YUMA_PATH_FUSED runs the single-read fused phase 1 (k_fused1)
- * wherever it applies (run outputs, 32 <= V <= 256, M % 4 == 0, M >= 256,
- * not Yuma2; measured slower at c2, kept for its experiments). Returns the
- * previous setting. Not thread-safe against concurrent launches.          */
-enum yuma_path { YUMA_PATH_AUTO = 0, YUMA_PATH_MULTIPASS = 1, YUMA_PATH_FUSED = 2 };
-int yuma_set_path(int path);
-
-/* Synchronous check of a workspace after a run has completed: 0 = clean,
- * 1 = a fused-phase-1 hand-off timed out (results invalid; a co-residency
- * failure, never expected on an idle device), < 0 = error.                 */
-int yuma_workspace_status(const void* workspace);
-/* Diagnostics after a completed run: out4 = {status, -, fused-phase-1 sweeps
- * that found their granule not yet published, polls they spent}.          */
-int yuma_workspace_counters(const void* workspace, unsigned* out4);
 
 const char* yuma_last_error(void);
 const char* yuma_version(void);

@@ -290,7 +290,7 @@ __device__ __forceinline__ void load4_vec(const float* __restrict__ v, int m, in
 // ---------------------------------------------------------------------------
 // Phase 1a: row sums (yumas.py:186 `W.sum(dim=1) + 1e-6`) and S / S.sum()
 // (yumas.py:189). One wave per row. Block x: (slice, 4-row block).
-// Summation order (shared with k_fused1, so both paths give the same bits):
+// Summation order:
 // the row is cut into 256-miner chunks; a chunk's partial is the balanced
 // binary tree over its 64 column quads of the sequential quad sums
 // ((x0+x1)+x2)+x3 (lane l holds quad l: the 64-lane butterfly); the chunk
@@ -755,7 +755,7 @@ constexpr int kHistWords = 4 * 16 * kHS;  // one block: 4 waves x 16 columns
 // The consensus search of this lane's 4 columns over the wave's normalised
 // validator rows (wn, s: rows rg + 16 i, padding rows hold wn = 0, s = 0).
 // `ut`: the slice's stakes in units of 2^-24 when they are exact (k_rowsum /
-// the fused reducer), else -1. `hb`: this wave's 16 x kHS histogram words.
+// its shard-stage twin), else -1. `hb`: this wave's 16 x kHS histogram words.
 // Returns k* per column (C_raw = k* 2^-iters), identical in the 16 lanes of a
 // column quad.
 // Reductions over the LPC lanes that share a column quad (LPC = 16: one DPP
@@ -1484,558 +1484,8 @@ __global__ __launch_bounds__(NT) void k_rank(
   if (threadIdx.x == 0) rpart[slice * tiles + tile] = ts;
 }
 
-// ---------------------------------------------------------------------------
-// Fused phase 1 (k_fused1): row sums, stake normalisation, consensus,
-// quantisation and rank (yumas.py:186-217; YumaRust :72-106, C in fp64) of
-// every slice in ONE read of W, for run outputs with 32 <= V <= 256.
-//
-// Geometry: one persistent block of 4 waves per CU (one wave per SIMD: the
-// whole 512-register file per lane). The T = ceil(M / 32) tiles of a slice
-// belong to a GROUP of T blocks: block j of a group owns miners
-// 32 j .. 32 j + 31 of every slice of the group, and group g takes the slices
-// g, g + G, g + 2G, ... of the chunk. Wave w owns 8 of the tile's miners;
-// lane (cq = lane / 32, rg = lane % 32) owns 4 of them in validator rows
-// rg + 32 r (r < 8), so every column reduction (consensus, rank) is a
-// 32-lane DPP/swizzle tree inside one wave, with no barrier.
-//
-// Cross-block data moves as tagged 8-byte granules {value, tag}
-// (cdna_hip_programming.md Guideline 16, R2: the data is the flag): the
-// producer writes each with ONE agent-scope (write-through) store and never
-// waits; the consumer sweeps them with agent-scope loads until every tag
-// matches. A hop costs two iterations: data published during iteration k is
-// swept at the end of iteration k + 1 (issued after everything else, so the
-// snapshot is a whole iteration old; its wait at the start of iteration k + 2
-// leaves the younger tile loads in flight) and used in iteration k + 2.
-// Stages of the i-th slice of a group:
-//   iteration i-1  L  load the tile (8 float4 per lane, registers)
-//   iteration i    P  row partials over the tile's 32 miners -> rowpart[i];
-//                     the raw tile moves to the LDS ring (4 x 32 KB)
-//   iteration i+2  D  block j sums its rows (j rpb .. j rpb + rpb - 1) over
-//                     the T partials in tile order, + 1e-6   -> rowsum[i]
-//   iteration i+4  C  S / sum S, the tile back from LDS, normalise,
-//                     consensus; tile sum of C_raw            -> cpart[i]
-//   iteration i+6  K  sum C over tiles, quantise own columns, clip, rank
-// The granules sit in rings of kF1Ring slots per group (tag = i + 1), zeroed
-// by a memset node before every launch. Every sweep is bounded: a timeout
-// raises ctl[1] (yuma_status reports it) instead of hanging the GPU.
-//
-// Summation orders are fixed (bitwise reproducible) and shared with the
-// multi-pass path: a row's tile partial is the balanced tree over the tile's
-// 8 column quads of the sequential quad sums (k_rowsum computes the same),
-// a row sum adds the tile partials in tile order, then 1e-6; sum S is
-// k_rowsum's lane-strided sum and butterfly.
-// ---------------------------------------------------------------------------
-constexpr int kF1Ring = 8;
-constexpr int kF1Tile = 32;              // miners per block tile
-constexpr int kF1R = 8;                  // validator rows per lane
-constexpr int kF1Slots = 4;              // LDS ring of raw tiles (P -> C)
-constexpr int kF1MaxBlocks = 256;        // persistent blocks (one per CU)
-constexpr unsigned kF1Spin = 1u << 22;   // polls (each after s_sleep) before giving up
-// LDS words: ring[4][4 waves][8 r][64 lanes][4] | hist | red[4][256] | dred[512]
-//            | rsd[256] | sn[256] | sraw[256] | cp[2][256] | misc[64]
-constexpr int kF1Ring0 = 0;
-constexpr int kF1Hist = kF1Slots * 4 * kF1R * 64 * 4;
-constexpr int kF1Red = kF1Hist + 4 * 8 * kHS;
-constexpr int kF1Dred = kF1Red + 4 * 256;
-constexpr int kF1Rsd = kF1Dred + 512;
-constexpr int kF1Sn = kF1Rsd + 256;
-constexpr int kF1Sraw = kF1Sn + 256;
-constexpr int kF1Cp = kF1Sraw + 256;
-constexpr int kF1Misc = kF1Cp + 512;
-constexpr int kF1Lds = kF1Misc + 64;
-static_assert(kF1Lds * 4 <= 160 * 1024, "k_fused1 LDS");
-
-struct F1Args {
-  const float* W;
-  const float* S;
-  const yuma_params_t* prm;
-  int N, V, M, T, G, rpb, nch, rust;
-  int s0, ns;
-  float* rsd;      // [slice][V] (absolute slice index)
-  float* sn;       // [slice][V]
-  int* sx;         // [slice]
-  float* C;        // [slice][M]
-  int* qlev;       // [slice][M]
-  float* R;        // [slice][M]
-  float* rpart;    // [slice][T]
-  float* sumc_f;   // [ns] (chunk-local slice index)
-  double* sumc_d;  // [ns]
-  unsigned long long* g_rowpart;  // [G][ring][T][V]
-  unsigned long long* g_rowsum;   // [G][ring][V]
-  unsigned long long* g_cpart;    // [G][ring][T][2]
-  unsigned* ctl;                  // [0] ticket, [1] timeout, [2..3] poll counters
-};
-
-typedef __attribute__((address_space(1))) unsigned long long g_u64;
-typedef __attribute__((address_space(1))) unsigned g_u32;
-
-__device__ __forceinline__ void put_granule(unsigned long long* p, unsigned tag, unsigned val) {
-  __hip_atomic_store((g_u64*)p, ((unsigned long long)tag << 32) | val, __ATOMIC_RELAXED,
-                     __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ unsigned long long get_granule(const unsigned long long* p) {
-  return __hip_atomic_load((const g_u64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// The value of a swept granule; polls again (bounded) while its tag is not
-// `tag` (the rare path: its loads wait for everything in flight).
-__device__ __forceinline__ unsigned settle(const unsigned long long* p, unsigned long long x,
-                                          unsigned tag, unsigned* ctl, unsigned& polls) {
-  if ((unsigned)(x >> 32) != tag) {
-    unsigned spins = 0;
-    do {
-      __builtin_amdgcn_s_sleep(2);
-      x = get_granule(p);
-      if (++spins > kF1Spin) {
-        __hip_atomic_store((g_u32*)(ctl + 1), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-    } while ((unsigned)(x >> 32) != tag);
-    polls += spins;
-  }
-  return (unsigned)x;
-}
-
-// Packed row division wn = RN(w / d) (div_fast_nz on pairs, lane-wide guard;
-// see load_norm_w); returns true when some operand is outside the guard.
-template <int R>
-__device__ __forceinline__ bool norm_packed(float (&wn)[R][4], const float (&d)[R]) {
-  typedef float f2 __attribute__((ext_vector_type(2)));
-  float amax = 0.0f, dmin = INFINITY;
-  unsigned ymin = 0xFFFFFFFFu;
-#pragma unroll
-  for (int i = 0; i < R; ++i) {
-    const float r = 1.0f / d[i];
-    amax = fmaxf(amax, fabsf(d[i]));
-    dmin = fminf(dmin, fabsf(d[i]));
-    const f2 r2 = {r, r}, nd2 = {-d[i], -d[i]};
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const f2 a2 = {wn[i][2 * h], wn[i][2 * h + 1]};
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        amax = fmaxf(amax, fabsf(a2[c]));
-        const unsigned y = (__float_as_uint(a2[c]) << 1) - 1u;
-        ymin = y < ymin ? y : ymin;
-      }
-      const f2 q = a2 * r2;
-      const f2 e = __builtin_elementwise_fma(nd2, q, a2);
-      const f2 q1 = __builtin_elementwise_fma(e, r2, q);
-      wn[i][2 * h] = q1[0];
-      wn[i][2 * h + 1] = q1[1];
-    }
-  }
-  return !(dmin >= 0x1p-60f && amax <= 0x1p60f &&
-           (ymin == 0xFFFFFFFFu || ymin + 1u >= (__float_as_uint(0x1p-60f) << 1)));
-}
-
-struct F1Ctx {
-  int V, M, T, G, rpb, nch, g, j, m, tid, lane, wave, cq, rg, nq, VM;
-  int dk0, dk1;  // this thread's D granule columns (row * V-offset resolved)
-  bool rust, small_idx, edge;
-  unsigned* lds;
-};
-// the swept granules of one iteration (issued at the end of the previous one)
-struct F1Sweep {
-  unsigned long long d0, d1, c, k0, k1;
-  float sraw;
-};
-
-__device__ __forceinline__ int f1_slice(const F1Args& A, const F1Ctx& c, int i) {
-  const int k = i < c.nq ? (i < 0 ? 0 : i) : c.nq - 1;
-  return A.s0 + c.g + c.G * k;
-}
-__device__ __forceinline__ int f1_ring(const F1Ctx& c, int i) {
-  return c.g * kF1Ring + ((i < 0 ? 0 : i) & (kF1Ring - 1));
-}
-__device__ __forceinline__ unsigned long long* f1_pD(const F1Args& A, const F1Ctx& c, int i, int dk) {
-  return A.g_rowpart + (long long)f1_ring(c, i) * c.T * c.V + dk;
-}
-__device__ __forceinline__ unsigned long long* f1_pC(const F1Args& A, const F1Ctx& c, int i) {
-  return A.g_rowsum + f1_ring(c, i) * c.V + min(c.tid, c.V - 1);
-}
-__device__ __forceinline__ unsigned long long* f1_pK(const F1Args& A, const F1Ctx& c, int i) {
-  return A.g_cpart + (f1_ring(c, i) * c.T + min(c.tid, c.T - 1)) * 2;
-}
-
-// Sweep loads of iteration i (D: rowpart of slice i-2, C: rowsum of slice
-// i-4 and its raw stakes, K: cpart of slice i-6), issued at the end of
-// iteration i-1.
-__device__ __forceinline__ void f1_sweep(const F1Args& A, const F1Ctx& c, int i, F1Sweep& w) {
-  const int nD = c.rpb * c.T;
-  w.d0 = w.d1 = w.c = w.k0 = w.k1 = 0;
-  w.sraw = 0.0f;
-  if (c.tid < nD) w.d0 = get_granule(f1_pD(A, c, i - 2, c.dk0));
-  if (c.tid + 256 < nD) w.d1 = get_granule(f1_pD(A, c, i - 2, c.dk1));
-  if (c.tid < c.V) {
-    w.c = get_granule(f1_pC(A, c, i - 4));
-    w.sraw = A.S[(long long)f1_slice(A, c, i - 4) * c.V + c.tid];
-  }
-  if (c.tid < c.T) {
-    w.k0 = get_granule(f1_pK(A, c, i - 6));
-    if (c.rust) w.k1 = get_granule(f1_pK(A, c, i - 6) + 1);
-  }
-}
-
-// branch-free tile loads (rows >= V and columns >= M read in-range
-// addresses and are zeroed later)
-__device__ __forceinline__ void f1_load(const F1Args& A, const F1Ctx& c, float (&t)[kF1R][4], int i) {
-  const float* Ws = A.W + (long long)f1_slice(A, c, i) * c.VM;
-  const int mm = c.m < c.M ? c.m : c.M - 4;
-#pragma unroll
-  for (int r = 0; r < kF1R; ++r) {
-    const int rr = min(c.rg + 32 * r, c.V - 1);
-    const float* p = c.small_idx ? Ws + ((unsigned)rr * (unsigned)c.M + (unsigned)mm)
-                                 : Ws + ((long long)rr * c.M + mm);
-    const fvec4 x = *reinterpret_cast<const fvec4*>(p);
-    t[r][0] = x.x;
-    t[r][1] = x.y;
-    t[r][2] = x.z;
-    t[r][3] = x.w;
-  }
-}
-__device__ __forceinline__ void f1_mask(const F1Ctx& c, float (&t)[kF1R][4]) {
-  if (!c.edge) return;  // block-uniform: only edge tiles hold padding
-#pragma unroll
-  for (int r = 0; r < kF1R; ++r)
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-      if (c.rg + 32 * r >= c.V || c.m + k >= c.M) t[r][k] = 0.0f;
-}
-// this wave's part of LDS ring slot `slot` (lane-contiguous float4 per row)
-__device__ __forceinline__ fvec4* f1_slot(const F1Ctx& c, int slot) {
-  return reinterpret_cast<fvec4*>(c.lds + kF1Ring0) + ((slot * 4 + c.wave) * kF1R) * 64 + c.lane;
-}
-
-// Iteration i; U = i mod 2 selects the register sets: tl[U ^ 1] receives
-// slice i+1, tl[U] holds slice i (P); tn[U] holds the normalised slice i-6
-// (K) and then receives slice i-4 (C).
-template <int U>
-__device__ __forceinline__ void f1_iter(const F1Args& A, const F1Ctx& c, int i, F1Sweep& w,
-                                        float (&tl)[2][kF1R][4], float (&tn)[2][kF1R][4],
-                                        float (&skeep)[2][kF1R], int (&hk)[2][4], unsigned& polls) {
-  constexpr int R = kF1R;
-  float* red = reinterpret_cast<float*>(c.lds + kF1Red);
-  float* dred = reinterpret_cast<float*>(c.lds + kF1Dred);
-  float* rsd_l = reinterpret_cast<float*>(c.lds + kF1Rsd);
-  float* sn_l = reinterpret_cast<float*>(c.lds + kF1Sn);
-  float* sraw_l = reinterpret_cast<float*>(c.lds + kF1Sraw);
-  unsigned* cp_l = c.lds + kF1Cp;
-  unsigned* misc = c.lds + kF1Misc;
-  const int tid = c.tid, V = c.V, T = c.T, nq = c.nq;
-  const bool doP = i < nq, doD = i >= 2 && i - 2 < nq, doC = i >= 4 && i - 4 < nq,
-             doK = i >= 6 && i - 6 < nq;
-  const int iD = i - 2, iC = i - 4, iK = i - 6;
-
-  // 1. the next tile
-  f1_load(A, c, tl[U ^ 1], i + 1);
-  // 2. settle this iteration's sweeps (older than the tile loads)
-  const int nD = c.rpb * T;
-  if (doD && tid < nD)
-    dred[tid] = __uint_as_float(settle(f1_pD(A, c, iD, c.dk0), w.d0, (unsigned)(iD + 1), A.ctl, polls));
-  if (doD && tid + 256 < nD)
-    dred[tid + 256] = __uint_as_float(settle(f1_pD(A, c, iD, c.dk1), w.d1, (unsigned)(iD + 1), A.ctl, polls));
-  if (doC && tid < V) {
-    rsd_l[tid] = __uint_as_float(settle(f1_pC(A, c, iC), w.c, (unsigned)(iC + 1), A.ctl, polls));
-    sraw_l[tid] = w.sraw;
-  }
-  if (doK && tid < T) {
-    cp_l[tid] = settle(f1_pK(A, c, iK), w.k0, (unsigned)(iK + 1), A.ctl, polls);
-    if (c.rust) cp_l[256 + tid] = settle(f1_pK(A, c, iK) + 1, w.k1, (unsigned)(iK + 1), A.ctl, polls);
-  }
-  // 3. P: row partials of tile i over its 32 miners
-  if (doP) {
-    f1_mask(c, tl[U]);
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const float a = ((tl[U][r][0] + tl[U][r][1]) + tl[U][r][2]) + tl[U][r][3];
-      const float b = a + __shfl_xor(a, 32, 64);  // the wave's two quads
-      if (c.cq == 0) red[c.wave * 256 + c.rg + 32 * r] = b;
-    }
-  }
-  __syncthreads();  // B1
-
-  // 4. publish P; D on wave 0; sum C (wave 2); S / sum S (wave 3)
-  if (doP && tid < V) {
-    const float part = (red[tid] + red[256 + tid]) + (red[512 + tid] + red[768 + tid]);
-    put_granule(A.g_rowpart + ((long long)f1_ring(c, i) * T + c.j) * V + tid, (unsigned)(i + 1),
-                __float_as_uint(part));
-  }
-  if (doD && c.wave == 0) {
-    // row sum = the 256-miner chunk partials (balanced tree over 8 tiles) in
-    // chunk order, + 1e-6 (k_rowsum's order). Lane L < rpb nch: chunk
-    // L % nch of own row L / nch.
-    const int nch = c.nch;
-    float cpv = 0.0f;
-    if (c.lane < c.rpb * nch) {
-      const int dr = c.lane / nch, ch = c.lane - dr * nch;
-      float p8[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const int t = ch * 8 + k;
-        p8[k] = t < T ? dred[dr * T + t] : 0.0f;
-      }
-      cpv = ((p8[0] + p8[1]) + (p8[2] + p8[3])) + ((p8[4] + p8[5]) + (p8[6] + p8[7]));
-    }
-    float mine = 0.0f;
-    for (int dr = 0; dr < c.rpb; ++dr) {
-      float acc = 0.0f;
-      for (int ch = 0; ch < nch; ++ch) acc = acc + __shfl(cpv, dr * nch + ch, 64);
-      mine = c.lane == dr ? acc : mine;
-    }
-    const int v = c.j * c.rpb + c.lane;
-    if (c.lane < c.rpb && v < V) {
-      const float rs = mine + 1e-6f;
-      put_granule(A.g_rowsum + f1_ring(c, iD) * V + v, (unsigned)(iD + 1), __float_as_uint(rs));
-      A.rsd[(long long)f1_slice(A, c, iD) * V + v] = rs;
-    }
-  }
-  if (doK && c.wave == 2) {
-    // sum C over tiles: lane-strided, then the wave butterfly (fixed order)
-    if (c.rust) {
-      double a = 0.0;
-      for (int t = c.lane; t < T; t += 64)
-        a = a + __hiloint2double((int)cp_l[256 + t], (int)cp_l[t]);
-      a = wave_sum_d(a);
-      if (c.lane == 0) {
-        misc[2] = (unsigned)__double2loint(a);
-        misc[3] = (unsigned)__double2hiint(a);
-      }
-    } else {
-      float a = 0.0f;
-      for (int t = c.lane; t < T; t += 64) a = a + __uint_as_float(cp_l[t]);
-      a = wave_sum(a);
-      if (c.lane == 0) misc[2] = __float_as_uint(a);
-    }
-  }
-  if (doC && c.wave == 3) {
-    // S / S.sum() (yumas.py:189) in k_rowsum's order, and the exact-stake
-    // units (or -1) of the consensus histogram finish
-    const int slC = f1_slice(A, c, iC);
-    float acc = 0.0f;
-    for (int v = c.lane; v < V; v += 64) acc = acc + sraw_l[v];
-    acc = wave_sum(acc);
-    int units = 0;
-    bool exact = true;
-    for (int v = c.lane; v < V; v += 64) {
-      const float q = sraw_l[v] / acc;
-      sn_l[v] = q;
-      if (c.j == 0) A.sn[(long long)slC * V + v] = q;
-      const float f = q * 16777216.0f;
-      exact &= f >= 0.0f && f <= 16777216.0f && __builtin_amdgcn_fractf(f) == 0.0f;
-      units += exact ? (int)f : 0;
-    }
-    for (int o = 1; o < 64; o <<= 1) units += __shfl_xor(units, o, 64);
-    exact = __all(exact) && units <= (1 << 24);
-    if (c.lane == 0) {
-      misc[4] = (unsigned)(exact ? units : -1);
-      if (c.j == 0) A.sx[slC] = exact ? units : -1;
-    }
-  }
-  __syncthreads();  // B2
-
-  // 5. K: quantise slice i-6's columns with sum C, clip, rank (tn[U])
-  if (doK) {
-    const int slK = f1_slice(A, c, iK);
-    const yuma_params_t& p = A.prm[slK % A.N];
-    float Cq[4];
-    int lev[4];
-    if (c.rust) {
-      const double sumd = __hiloint2double((int)misc[3], (int)misc[2]);
-      const double it = 1.0 / (double)(1 << p.bisect_iters);  // exact (power of two)
-#pragma unroll
-      for (int k = 0; k < 4; ++k) lev[k] = (int)((double)hk[U][k] * it / sumd * 65535.0);
-    } else {
-      const RowDiv sd = row_div(__uint_as_float(misc[2]));
-      const float it = 1.0f / (float)(1 << p.bisect_iters);  // exact (power of two)
-#pragma unroll
-      for (int k = 0; k < 4; ++k) lev[k] = (int)(div_rn((float)hk[U][k] * it, sd) * 65535.0f);
-    }
-    const RowDiv q65535 = row_div(65535.0f);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) Cq[k] = c.m + k < c.M ? div_rn((float)lev[k], q65535) : 0.0f;
-    float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-    for (int r = 0; r < R; ++r)
-#pragma unroll
-      for (int k = 0; k < 4; ++k) acc[k] = acc[k] + skeep[U][r] * vmin(tn[U][r][k], Cq[k]);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) acc[k] = red_sum<32>(acc[k]);
-    if (c.rg == 0 && c.m < c.M) {
-      const long long o = (long long)slK * c.M + c.m;
-      *reinterpret_cast<fvec4*>(A.R + o) = fvec4{acc[0], acc[1], acc[2], acc[3]};
-      *reinterpret_cast<fvec4*>(A.C + o) = fvec4{Cq[0], Cq[1], Cq[2], Cq[3]};
-      *reinterpret_cast<int4*>(A.qlev + o) = make_int4(lev[0], lev[1], lev[2], lev[3]);
-    }
-    float ws = ((acc[0] + acc[1]) + acc[2]) + acc[3];
-    ws = ws + __shfl_xor(ws, 32, 64);
-    if (c.lane == 0) misc[32 + c.wave] = __float_as_uint(ws);
-  }
-  // 6. C: slice i-4 back from the ring, normalise, consensus (into tn[U])
-  if (doC) {
-    const int slC = f1_slice(A, c, iC);
-    const yuma_params_t& p = A.prm[slC % A.N];
-    const fvec4* src = f1_slot(c, iC & (kF1Slots - 1));
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const fvec4 x = src[r * 64];
-      tn[U][r][0] = x.x;
-      tn[U][r][1] = x.y;
-      tn[U][r][2] = x.z;
-      tn[U][r][3] = x.w;
-    }
-    float d[R], s[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const int row = c.rg + 32 * r, rr = min(row, V - 1);
-      d[r] = rsd_l[rr];
-      s[r] = row < V ? sn_l[rr] : 0.0f;
-    }
-    if (__any(norm_packed<R>(tn[U], d))) {  // rare: IEEE division from W
-      f1_load(A, c, tn[U], iC);
-#pragma unroll
-      for (int r = 0; r < R; ++r)
-#pragma unroll
-        for (int k = 0; k < 4; ++k) tn[U][r][k] = tn[U][r][k] / d[r];
-    }
-    f1_mask(c, tn[U]);
-    const int ut = (p.flags & YUMA_FLAG_NO_HIST) ? -1 : (int)misc[4];
-    int hi[4];
-    consensus_search<R, 32>(tn[U], s, p.kappa, p.bisect_iters, ut, c.lds + kF1Hist + c.wave * 8 * kHS,
-                            c.lane, c.cq, c.rg, hi);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) hk[U][k] = hi[k];
-#pragma unroll
-    for (int r = 0; r < R; ++r) skeep[U][r] = s[r];
-    // tile partial of C_raw (quads sequential, the two quads, waves below)
-    if (c.rust) {
-      const double it = 1.0 / (double)(1 << p.bisect_iters);
-      double a = 0.0;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) a = a + (c.m + k < c.M ? (double)hi[k] * it : 0.0);
-      a = a + __shfl_xor(a, 32, 64);
-      if (c.lane == 0) {
-        misc[16 + 2 * c.wave] = (unsigned)__double2loint(a);
-        misc[17 + 2 * c.wave] = (unsigned)__double2hiint(a);
-      }
-    } else {
-      const float it = 1.0f / (float)(1 << p.bisect_iters);
-      float a = 0.0f;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) a = a + (c.m + k < c.M ? (float)hi[k] * it : 0.0f);
-      a = a + __shfl_xor(a, 32, 64);
-      if (c.lane == 0) misc[16 + c.wave] = __float_as_uint(a);
-    }
-  }
-  // 7. the raw tile i into the ring (its slot held slice i-4, read above by
-  //    this same wave: each wave owns its part of a slot)
-  if (doP) {
-    fvec4* dst = f1_slot(c, i & (kF1Slots - 1));
-#pragma unroll
-    for (int r = 0; r < R; ++r) dst[r * 64] = fvec4{tl[U][r][0], tl[U][r][1], tl[U][r][2], tl[U][r][3]};
-  }
-  __syncthreads();  // B3
-  if (doC && tid == 0) {
-    unsigned long long* pc = A.g_cpart + (f1_ring(c, iC) * T + c.j) * 2;
-    if (c.rust) {
-      double q[4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) q[k] = __hiloint2double((int)misc[17 + 2 * k], (int)misc[16 + 2 * k]);
-      const double a = (q[0] + q[1]) + (q[2] + q[3]);
-      put_granule(pc, (unsigned)(iC + 1), (unsigned)__double2loint(a));
-      put_granule(pc + 1, (unsigned)(iC + 1), (unsigned)__double2hiint(a));
-    } else {
-      float q[4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) q[k] = __uint_as_float(misc[16 + k]);
-      put_granule(pc, (unsigned)(iC + 1), __float_as_uint((q[0] + q[1]) + (q[2] + q[3])));
-    }
-  }
-  if (doK && tid == 64) {
-    const int slK = f1_slice(A, c, iK);
-    float q[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) q[k] = __uint_as_float(misc[32 + k]);
-    A.rpart[(long long)slK * T + c.j] = (q[0] + q[1]) + (q[2] + q[3]);
-    if (c.j == 0) {
-      const int ls = slK - A.s0;
-      if (c.rust) {
-        const double sd = __hiloint2double((int)misc[3], (int)misc[2]);
-        A.sumc_d[ls] = sd;
-        A.sumc_f[ls] = (float)sd;
-      } else {
-        A.sumc_f[ls] = __uint_as_float(misc[2]);
-      }
-    }
-  }
-  // 8. the sweeps of iteration i+1: a whole iteration after their producers
-  f1_sweep(A, c, i + 1, w);
-}
-
-__global__ __launch_bounds__(256, 1) void k_fused1(F1Args A) {
-  __shared__ __attribute__((aligned(16))) unsigned lds[kF1Lds];
-  F1Ctx c;
-  c.tid = threadIdx.x;
-  c.lane = c.tid & 63;
-  c.wave = c.tid >> 6;
-  c.cq = c.lane >> 5;
-  c.rg = c.lane & 31;
-  c.lds = lds;
-  if (c.tid == 0)
-    lds[kF1Misc] = __hip_atomic_fetch_add((g_u32*)A.ctl, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __syncthreads();
-  const int ticket = (int)lds[kF1Misc];
-  c.V = A.V;
-  c.M = A.M;
-  c.T = A.T;
-  c.G = A.G;
-  c.rpb = A.rpb;
-  c.nch = A.nch;
-  c.g = ticket / A.T;
-  c.j = ticket - c.g * A.T;
-  if (c.g >= A.G) return;  // the whole block (uniform)
-  c.nq = (A.ns - c.g + A.G - 1) / A.G;
-  if (c.nq <= 0) return;
-  c.VM = A.V * A.M;
-  c.m = c.j * kF1Tile + c.wave * 8 + c.cq * 4;
-  c.rust = A.rust != 0;
-  c.small_idx = c.VM < (1 << 30);
-  c.edge = A.V < 256 || (c.j + 1) * kF1Tile > A.M;
-  // D granule columns: entry k = (own row k / T, tile k % T)
-  c.dk0 = (c.tid % A.T) * A.V + min(c.j * A.rpb + c.tid / A.T, A.V - 1);
-  c.dk1 = ((c.tid + 256) % A.T) * A.V + min(c.j * A.rpb + (c.tid + 256) / A.T, A.V - 1);
-  float tl[2][kF1R][4];
-  float tn[2][kF1R][4];
-  float skeep[2][kF1R];
-  int hk[2][4];
-  unsigned polls = 0;
-  F1Sweep w;
-  f1_load(A, c, tl[0], 0);
-  f1_sweep(A, c, 0, w);
-  for (int i0 = 0;; i0 += 2) {
-    f1_iter<0>(A, c, i0, w, tl, tn, skeep, hk, polls);
-    f1_iter<1>(A, c, i0 + 1, w, tl, tn, skeep, hk, polls);
-    if (i0 + 2 > c.nq + 5) break;
-  }
-  // diagnostics: one add per wave that polled
-  const unsigned wp = (unsigned)__reduce_add_sync(~0ull, (int)polls);
-  if (c.lane == 0 && wp != 0u) {
-    __hip_atomic_fetch_add((g_u32*)(A.ctl + 2), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_fetch_add((g_u32*)(A.ctl + 3), wp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
-// fault[0] |= the fused kernel's timeout word (sticky over the chunks of a run)
-// fault[2..3] += the sweeps that had to poll and their polls (diagnostics)
-__global__ void k_fault(const unsigned* __restrict__ ctl, unsigned* __restrict__ fault) {
-  if (threadIdx.x == 0) {
-    if (ctl[1] != 0u) fault[0] = 1u;
-    fault[2] += ctl[2];
-    fault[3] += ctl[3];
-  }
-}
-
-// Liquid alpha only (the fused phase 1 already quantised C): quantiles of the
-// levels and bond_alpha[m] (yumas.py:231-253). One block per slice.
+// Liquid alpha only (a miner-column-sharded run quantised C per shard): quantiles of
+// the levels and bond_alpha[m] (yumas.py:231-253). One block per slice.
 template <int NT>
 __global__ __launch_bounds__(NT) void k_liquid(const yuma_params_t* __restrict__ prm, int N, int M,
                                                long long slice0, const float* __restrict__ C,
@@ -2730,9 +2180,8 @@ int fail(int code, const char* fmt, ...) {
 size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
 struct Workspace {
-  unsigned* fault;  // [4] at offset 0: [0] a fused-phase-1 sweep timed out (sticky per run)
   float* rsd;
-  int* sx;  // per slice: exact stake units or -1 (k_rowsum / k_fused1)
+  int* sx;  // per slice: exact stake units or -1 (k_rowsum)
   float* sn;
   double* craw;
   int* qlev;
@@ -2748,24 +2197,8 @@ struct Workspace {
   float* Bstate;
   float* sumc_f;
   double* sumc_d;
-  unsigned* f1;     // fused phase 1: ctl[4], then the granule rings (memset per launch)
-  size_t f1_bytes;  // bytes reserved for ctl + rings
   size_t bytes;
 };
-
-// Granule rings of k_fused1 for G groups of T blocks (G * T <= kF1MaxBlocks).
-struct F1Rings {
-  size_t rowpart, rowsum, cpart, total;  // byte offsets from ws.f1, total bytes
-};
-F1Rings f1_rings(int G, int T, int V) {
-  F1Rings r{};
-  const size_t slots = (size_t)G * yk::kF1Ring;
-  r.rowpart = 64;  // after ctl[4] (padded)
-  r.rowsum = r.rowpart + slots * T * V * 8;
-  r.cpart = r.rowsum + slots * V * 8;
-  r.total = (r.cpart + slots * T * 2 * 8 + 15) & ~size_t(15);
-  return r;
-}
 
 Workspace carve(char* base, int variant, int N, int E, int V, int M, int full) {
   (void)variant;
@@ -2778,7 +2211,6 @@ Workspace carve(char* base, int variant, int N, int E, int V, int M, int full) {
     off += align256(bytes);
     return p;
   };
-  w.fault = (unsigned*)take(16);
   w.rsd = (float*)take(S * V * 4);
   w.sx = (int*)take(S * 4);
   w.sn = (float*)take(S * V * 4);
@@ -2788,7 +2220,7 @@ Workspace carve(char* base, int variant, int N, int E, int V, int M, int full) {
   w.R = (float*)take(S * M * 4);
   w.I = (float*)take(S * M * 4);
   w.ba = (float*)take(S * M * 4);
-  w.rpart = (float*)take(S * (size_t)((M + yk::kF1Tile - 1) / yk::kF1Tile) * 4);
+  w.rpart = (float*)take(S * tiles * 4);
   w.dpart = (float*)take(S * tiles * V * 4);
   w.scal = (float*)take(S * 8 * 4);
   w.tvc = full ? (float*)take(S * tiles * V * 4) : nullptr;
@@ -2796,14 +2228,6 @@ Workspace carve(char* base, int variant, int N, int E, int V, int M, int full) {
   w.Bstate = (float*)take((size_t)N * V * M * 4);
   w.sumc_f = (float*)take(S * 4);
   w.sumc_d = (double*)take(S * 8);
-  // rings sized for the largest group count any grid of kF1MaxBlocks can form
-  w.f1_bytes = 0;
-  const size_t ftiles = (size_t)(M + yk::kF1Tile - 1) / yk::kF1Tile;
-  if (V <= 256 && ftiles <= (size_t)yk::kF1MaxBlocks) {
-    const int T = (int)ftiles;
-    w.f1_bytes = f1_rings(yk::kF1MaxBlocks / T, T, V).total;
-  }
-  w.f1 = w.f1_bytes ? (unsigned*)take(w.f1_bytes) : nullptr;
   w.bytes = off;
   return w;
 }
@@ -2869,18 +2293,6 @@ void launch_consensus(RowCfg rc, long long nblocks, hipStream_t st, const float*
                 slice0, tiles, craw, P);
       break;
   }
-}
-
-int device_cus() {
-  static int cus = 0;
-  if (cus == 0) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        cus <= 0)
-      cus = 1;
-  }
-  return cus;
 }
 
 template <bool VEC>
@@ -3011,31 +2423,6 @@ struct PhaseTimer {
   }
 };
 
-// Which phase-1 path run_impl takes (yuma_set_path; tests compare them).
-int g_path = YUMA_PATH_AUTO;
-
-int fused_blocks() {
-  const int cus = device_cus();
-  return cus < yk::kF1MaxBlocks ? cus : yk::kF1MaxBlocks;
-}
-
-// k_fused1 (opt-in, YUMA_PATH_FUSED) serves run outputs of 32 <= V <= 256
-// validators on float4 rows with whole tile groups resident (T <= one block
-// per CU); Yuma2 (which clips the previous epoch's weights), the full-output
-// dicts of the epoch functions and small subnets take the multi-pass
-// kernels. Measured slower than the multi-pass path at c2 (5.4 vs 2.3 ms for
-// phase 1): one wave per SIMD leaves it VALU-issue
-// bound, and the 128 blocks of a group drift past the hand-offs' lag.
-bool fused_eligible(int variant, int N, int E, int V, int M, bool vec, const yuma_outputs_t* out,
-                    int full) {
-  if (g_path != YUMA_PATH_FUSED) return false;
-  if (!vec || variant == YUMA_VARIANT_YUMA2 || full) return false;
-  if (V < 32 || V > 256 || M < 256) return false;
-  if (out->Wn || out->Wc || out->P || out->T) return false;
-  if ((long long)N * E > (1ll << 30)) return false;  // int slice indices
-  return (M + yk::kF1Tile - 1) / yk::kF1Tile <= fused_blocks();
-}
-
 int run_impl(int variant, const yuma_params_t* prm, int N, int E, int V, int M, const float* W,
              const float* S, const float* B_init, const float* Wprev_init,
              const yuma_outputs_t* out, void* workspace, size_t ws_bytes, int chunk,
@@ -3073,7 +2460,6 @@ int run_impl(int variant, const yuma_params_t* prm, int N, int E, int V, int M, 
   // liquid bond_alpha lives in the caller's buffer when requested; scenarios
   // with liquid_mode OFF neither write nor read it
   float* ba_buf = out->bond_alpha ? out->bond_alpha : ws.ba;
-  const bool fused = fused_eligible(variant, N, E, V, M, vec, out, full) && ws.f1 != nullptr;
 
   // one chunk by default: phase 1 of every epoch, then one bond scan
   if (chunk <= 0 || chunk > E) chunk = E;
@@ -3084,53 +2470,12 @@ int run_impl(int variant, const yuma_params_t* prm, int N, int E, int V, int M, 
   PhaseTimer tm{};
   tm.ms = phase_ms;
   tm.st = st;
-  (void)hipMemsetAsync(ws.fault, 0, 16, st);
 
   for (int c0 = 0; c0 < E; c0 += chunk) {
     const int c1 = c0 + chunk < E ? c0 + chunk : E;
     const long long s0 = (long long)c0 * N;
     const long long ns = (long long)(c1 - c0) * N;
-    if (fused) {
-      tm.mark(YUMA_PHASE_FUSED1);
-      const int T = (M + yk::kF1Tile - 1) / yk::kF1Tile;
-      long long G = fused_blocks() / T;
-      if (G > ns) G = ns;
-      const F1Rings rg = f1_rings((int)G, T, V);
-      char* f1 = (char*)ws.f1;
-      yk::F1Args A{};
-      A.W = W;
-      A.S = S;
-      A.prm = prm;
-      A.N = N;
-      A.V = V;
-      A.M = M;
-      A.T = T;
-      A.G = (int)G;
-      A.rpb = (V + T - 1) / T;
-      A.nch = (T + 7) / 8;
-      A.rust = variant == YUMA_VARIANT_RUST;
-      A.s0 = (int)s0;
-      A.ns = (int)ns;
-      A.rsd = ws.rsd;
-      A.sn = ws.sn;
-      A.sx = ws.sx;
-      A.C = C;
-      A.qlev = ws.qlev;
-      A.R = Rr;
-      A.rpart = ws.rpart;
-      A.sumc_f = ws.sumc_f;
-      A.sumc_d = ws.sumc_d;
-      A.g_rowpart = (unsigned long long*)(f1 + rg.rowpart);
-      A.g_rowsum = (unsigned long long*)(f1 + rg.rowsum);
-      A.g_cpart = (unsigned long long*)(f1 + rg.cpart);
-      A.ctl = ws.f1;
-      (void)hipMemsetAsync(ws.f1, 0, rg.total, st);  // tickets, tags: re-initialised every launch
-      YK_LAUNCH(yk::k_fused1, G * T, 256, st, A);
-      YK_LAUNCH(yk::k_fault, 1, 64, st, ws.f1, ws.fault);
-      tm.mark(YUMA_PHASE_LIQUID);
-      YK_LAUNCH(yk::k_liquid<256>, ns, 256, st, prm, N, M, s0, C, ws.qlev, M, ba_buf, ws.scal,
-                ws.sumc_f, ws.sumc_d, variant == YUMA_VARIANT_RUST ? 1 : 0);
-    } else {
+    {
       const int rowblocks4 = (V + 3) / 4;
       tm.mark(YUMA_PHASE_ROWSUM);
       if (vec)
@@ -3160,8 +2505,7 @@ int run_impl(int variant, const yuma_params_t* prm, int N, int E, int V, int M, 
                            out->Wn, out->Wc, ws.tvc, ws.tvn);
     }
     tm.mark(YUMA_PHASE_INCENTIVE);
-    const int rtiles = fused ? (M + yk::kF1Tile - 1) / yk::kF1Tile : tiles;  // rank partials per slice
-    YK_LAUNCH(yk::k_incentive, ns, 256, st, Rr, ws.rpart, out->P, M, s0, rtiles, I,
+    YK_LAUNCH(yk::k_incentive, ns, 256, st, Rr, ws.rpart, out->P, M, s0, tiles, I,
               out->P ? out->T : nullptr, ws.scal, nullptr);
 
     yk::BondArgs A{};
@@ -3476,29 +2820,6 @@ int yuma_graph_destroy(yuma_graph_t graph) {
   (void)hipGraphDestroy(graph->graph);
   delete graph;
   return YUMA_OK;
-}
-
-int yuma_set_path(int path) {
-  if (path != YUMA_PATH_AUTO && path != YUMA_PATH_MULTIPASS && path != YUMA_PATH_FUSED)
-    return fail(YUMA_EINVAL, "unknown path %d", path);
-  const int prev = g_path;
-  g_path = path;
-  return prev;
-}
-
-int yuma_workspace_counters(const void* workspace, unsigned* out4) {
-  if (workspace == nullptr || out4 == nullptr) return fail(YUMA_EINVAL, "NULL argument");
-  if (hipMemcpy(out4, workspace, 16, hipMemcpyDeviceToHost) != hipSuccess)
-    return fail(YUMA_EHIP, "reading the workspace counters failed");
-  return YUMA_OK;
-}
-
-int yuma_workspace_status(const void* workspace) {
-  if (workspace == nullptr) return fail(YUMA_EINVAL, "NULL workspace");
-  unsigned f = 0;
-  if (hipMemcpy(&f, workspace, sizeof f, hipMemcpyDeviceToHost) != hipSuccess)
-    return fail(YUMA_EHIP, "reading the workspace status failed");
-  return (int)f;
 }
 
 const char* yuma_last_error(void) { return g_err; }

@@ -29,11 +29,9 @@ _PKG_ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__fi
 LIB_PATH = os.environ.get("YUMA_HIP_LIB", os.path.join(_PKG_ROOT, "lib", LIB_NAME))
 
 VARIANT_RUST, VARIANT_YUMA1, VARIANT_YUMA2, VARIANT_YUMA3, VARIANT_YUMA4 = range(5)
-PHASES = ("rowsum", "consensus", "quantise", "rank", "incentive", "bonds", "finalize",
-          "fused1", "liquid")
+PHASES = ("rowsum", "consensus", "quantise", "rank", "incentive", "bonds", "finalize")
 FLAG_NO_HIST = 1  # yuma_params_t.flags: plain bisection instead of the histogram finish
 FLAG_RESET_ALL_COLUMNS = 2  # the reset zeroes every column (reset_bonds_index None)
-PATH_AUTO, PATH_MULTIPASS, PATH_FUSED = 0, 1, 2
 RESET_NONE, RESET_ALWAYS, RESET_IF_ZERO_CONSENSUS = range(3)
 LIQUID_OFF, LIQUID_QUANTILE, LIQUID_CONST_AB = range(3)
 OVR_HIGH, OVR_LOW, OVR_FORCE_Q99 = 1, 2, 4
@@ -49,9 +47,6 @@ EXPORTED_SYMBOLS = (
     "yuma_graph_launch",
     "yuma_graph_nodes",
     "yuma_graph_destroy",
-    "yuma_set_path",
-    "yuma_workspace_status",
-    "yuma_workspace_counters",
     "yuma_last_error",
     "yuma_version",
 )
@@ -159,12 +154,6 @@ def load_library(path: str | None = None):
         lib.yuma_graph_nodes.restype = i32
         lib.yuma_graph_destroy.argtypes = [vp]
         lib.yuma_graph_destroy.restype = i32
-        lib.yuma_set_path.argtypes = [i32]
-        lib.yuma_set_path.restype = i32
-        lib.yuma_workspace_status.argtypes = [vp]
-        lib.yuma_workspace_status.restype = i32
-        lib.yuma_workspace_counters.argtypes = [vp, ctypes.POINTER(ctypes.c_uint32)]
-        lib.yuma_workspace_counters.restype = i32
         lib.yuma_last_error.argtypes = []
         lib.yuma_last_error.restype = ctypes.c_char_p
         lib.yuma_version.argtypes = []
@@ -481,34 +470,6 @@ def synth_weights(seed: int, E: int, N: int, V: int, M: int, t0: int = 0,
     _check(load_library().yuma_synth_weights(int(seed) & 0xFFFFFFFFFFFFFFFF, E, N, V, M, t0,
                                              out.data_ptr(), stream), "yuma_synth_weights")
     return out
-
-
-def set_path(path: int) -> int:
-    """Phase-1 path for this process: PATH_AUTO / PATH_MULTIPASS (the
-    multi-pass kernels) or PATH_FUSED (the single-read fused kernel where it
-    applies). Returns the previous setting."""
-    rc = load_library().yuma_set_path(int(path))
-    if rc < 0:
-        _check(rc, "yuma_set_path")
-    return rc
-
-
-def workspace_status(result: "RunResult") -> int:
-    """0 when the run that produced `result` completed cleanly; 1 when a
-    fused phase-1 hand-off timed out (its outputs are invalid). Synchronous."""
-    ws = result.extra["_inputs"][5]
-    rc = load_library().yuma_workspace_status(ctypes.c_void_p(ws.data_ptr()))
-    if rc < 0:
-        _check(rc, "yuma_workspace_status")
-    return rc
-
-
-def workspace_counters(ws: torch.Tensor) -> list[int]:
-    """[status, -, fused sweeps that polled, polls] of a workspace (diagnostics)."""
-    buf = (ctypes.c_uint32 * 4)()
-    _check(load_library().yuma_workspace_counters(ctypes.c_void_p(ws.data_ptr()), buf),
-           "yuma_workspace_counters")
-    return list(buf)
 
 
 def version() -> str:
