@@ -92,6 +92,42 @@ __global__ __launch_bounds__(256) void k_scan(const fvec4* __restrict__ x, fvec4
   }
 }
 
+// the scan with R rows per thread (a block owns 16 R rows of the tile)
+template <int P, int R, bool NT>
+__global__ __launch_bounds__(256) void k_scan_r(const fvec4* __restrict__ x, fvec4* __restrict__ y, int steps, int V,
+                                                int M) {
+  const int tiles = M / 64;
+  const int tile = blockIdx.x % tiles, rb = blockIdx.x / tiles;
+  const int c4 = threadIdx.x & 15;
+  const long long m4 = (long long)M / 4;
+  const long long sl = (long long)V * m4;
+  long long off[R];
+#pragma unroll
+  for (int i = 0; i < R; ++i) off[i] = (long long)(rb * 16 * R + (threadIdx.x >> 4) + 16 * i) * m4 + tile * 16 + c4;
+  fvec4 ring[P][R];
+  fvec4 acc[R];
+#pragma unroll
+  for (int i = 0; i < R; ++i) acc[i] = fvec4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int k = 0; k < P; ++k)
+#pragma unroll
+    for (int i = 0; i < R; ++i) ring[k][i] = x[k * sl + off[i]];
+  for (int t0 = 0; t0 < steps; t0 += P) {
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+      const int t = t0 + k;
+      if (t >= steps) break;
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        acc[i] = acc[i] * 0.5f + ring[k][i];
+        if (NT) __builtin_nontemporal_store(acc[i], y + t * sl + off[i]);
+        else y[t * sl + off[i]] = acc[i];
+        if (t + P < steps) ring[k][i] = x[(t + P) * sl + off[i]];
+      }
+    }
+  }
+}
+
 template <typename F>
 static float time_ms(int reps, F f) {
   hipEvent_t a, b;
@@ -158,6 +194,11 @@ int main() {
     rep("scan P4 nt", 2 * B * 1000 / 1024, time_ms(reps, [&] { hipLaunchKernelGGL((k_scan<4, true>), dim3(g), dim3(256), 0, 0, x, y, steps, V, M); }));
     rep("scan P8 nt", 2 * B * 1000 / 1024, time_ms(reps, [&] { hipLaunchKernelGGL((k_scan<8, true>), dim3(g), dim3(256), 0, 0, x, y, steps, V, M); }));
     rep("scan P16 nt", 2 * B * 1000 / 1024, time_ms(reps, [&] { hipLaunchKernelGGL((k_scan<16, true>), dim3(g), dim3(256), 0, 0, x, y, steps, V, M); }));
+    rep("scan R2 P4", 2 * B * 1000 / 1024, time_ms(reps, [&] { hipLaunchKernelGGL((k_scan_r<4, 2, false>), dim3(g / 2), dim3(256), 0, 0, x, y, steps, V, M); }));
+    rep("scan R2 P4 nt", 2 * B * 1000 / 1024, time_ms(reps, [&] { hipLaunchKernelGGL((k_scan_r<4, 2, true>), dim3(g / 2), dim3(256), 0, 0, x, y, steps, V, M); }));
+    rep("scan R2 P8 nt", 2 * B * 1000 / 1024, time_ms(reps, [&] { hipLaunchKernelGGL((k_scan_r<8, 2, true>), dim3(g / 2), dim3(256), 0, 0, x, y, steps, V, M); }));
+    rep("scan R4 P4 nt", 2 * B * 1000 / 1024, time_ms(reps, [&] { hipLaunchKernelGGL((k_scan_r<4, 4, true>), dim3(g / 4), dim3(256), 0, 0, x, y, steps, V, M); }));
+    rep("scan R1 P8", 2 * B * 1000 / 1024, time_ms(reps, [&] { hipLaunchKernelGGL((k_scan_r<8, 1, false>), dim3(g), dim3(256), 0, 0, x, y, steps, V, M); }));
   }
   return 0;
 }

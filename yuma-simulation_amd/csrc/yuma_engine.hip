@@ -1869,7 +1869,7 @@ __global__ __launch_bounds__(NT) void k_bonds(BondArgs A) {
 // (a register ring refilled as each epoch is consumed), so the per-epoch HBM
 // latency is hidden behind P-1 epochs of work.
 // ---------------------------------------------------------------------------
-template <int VARIANT, int R, bool VEC, int P, bool VECI>
+template <int VARIANT, int R, bool VEC, int P, bool VECI, bool NT = false>
 __global__ __launch_bounds__(256) void k_bonds_elem(BondArgs A) {
   constexpr int G = 16;
   const Lay L = lay();
@@ -1984,13 +1984,21 @@ __global__ __launch_bounds__(256) void k_bonds_elem(BondArgs A) {
             B[i][c] = tmin(nb, 1.0f);
           }
         }
-        if (A.B_hist != nullptr && row < V)
-          store4<VEC>(A.B_hist + slice * VM + (long long)row * M, m, M, B[i]);
+        if (A.B_hist != nullptr && row < V) {
+          float* hp = A.B_hist + slice * VM + (long long)row * M;
+          if (NT && VEC) {  // write-once history: non-temporal stores
+            if (m < M)
+              __builtin_nontemporal_store(fvec4{B[i][0], B[i][1], B[i][2], B[i][3]},
+                                          reinterpret_cast<fvec4*>(hp + m));
+          } else {
+            store4<VEC>(hp, m, M, B[i]);
+          }
+        }
         float d = 0.0f;
 #pragma unroll
         for (int c = 0; c < 4; ++c)
           if (m + c < M) d = d + B[i][c] * ri[k][c];
-        d = sum_row16(d);
+        d = wsum16(d);  // sum_row16's xor-butterfly tree, on DPP
         if (L.c4 == 0 && row < V) A.dpart[(slice * A.tiles + tile) * V + row] = d;
       }
       has_old = true;
@@ -2366,17 +2374,20 @@ void launch_bonds_colnorm(RowCfg rc, long long nblocks, hipStream_t st, const yk
   }
 }
 
-// Element-wise variants: 256 threads, one row x 4 miners per thread (16-row
-// blocks), the inputs of the next 4 epochs kept in flight. Measured on
-// MI355X (c2 / c3): per-column incentive / bond_alpha loads are faster while
-// the bond history is written (1.73 vs 1.92 ms), float4 ones without it
-// (1.11 vs 1.28 ms at c2, 18.0 vs 26.8 ms at c3).
+// Element-wise variants (Yuma3 / Yuma4): 256 threads, R rows x 4 miners per
+// thread (16 R-row blocks), the inputs of the next P epochs in flight, float4
+// incentive / bond_alpha loads. Measured on MI355X at c2 (tools/ab_bonds.sh,
+// DESIGN.md section 2): writing the bond history, R = 2, P = 2 with
+// non-temporal history stores (Yuma3 1.68 ms, Yuma4 liquid 1.72 ms, against
+// 1.81 / 2.66 for R = 1, P = 4 and per-column loads); without the history,
+// R = 1, P = 4 (1.13 ms vs 1.36 for R = 2).
+int bonds_rows(bool vec, bool hist) { return vec && hist ? 2 : 1; }
 template <int VARIANT, bool VEC>
 void launch_bonds_elem(long long nblocks, hipStream_t st, const yk::BondArgs& A) {
-  if (A.B_hist == nullptr)
-    YK_LAUNCH((yk::k_bonds_elem<VARIANT, 1, VEC, 4, VEC>), nblocks, 256, st, A);
+  if (bonds_rows(VEC, A.B_hist != nullptr) == 2)
+    YK_LAUNCH((yk::k_bonds_elem<VARIANT, 2, VEC, 2, VEC, true>), nblocks, 256, st, A);
   else
-    YK_LAUNCH((yk::k_bonds_elem<VARIANT, 1, VEC, 4, false>), nblocks, 256, st, A);
+    YK_LAUNCH((yk::k_bonds_elem<VARIANT, 1, VEC, 4, VEC, false>), nblocks, 256, st, A);
 }
 
 template <bool VEC>
@@ -2465,7 +2476,8 @@ int run_impl(int variant, const yuma_params_t* prm, int N, int E, int V, int M, 
   if (chunk <= 0 || chunk > E) chunk = E;
 
   const int colnorm = variant <= YUMA_VARIANT_YUMA2;
-  const int rowblocks = colnorm ? 1 : (V + 15) / 16;
+  const int brows = 16 * bonds_rows(vec, out->B_hist != nullptr);  // rows per bond block
+  const int rowblocks = colnorm ? 1 : (V + brows - 1) / brows;
 
   PhaseTimer tm{};
   tm.ms = phase_ms;
@@ -2677,7 +2689,8 @@ int shard_stage_impl(int stage, int variant, const yuma_params_t* prm, int N, in
       A.V = V;
       A.M = M;
       A.tiles = tiles;
-      A.rowblocks = variant <= YUMA_VARIANT_YUMA2 ? 1 : (V + 15) / 16;
+      const int brows = 16 * bonds_rows(vec, out->B_hist != nullptr);
+      A.rowblocks = variant <= YUMA_VARIANT_YUMA2 ? 1 : (V + brows - 1) / brows;
       A.t0 = 0;
       A.t1 = E;
       const long long nb = (long long)N * tiles * A.rowblocks;
