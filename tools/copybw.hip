@@ -128,6 +128,60 @@ __global__ __launch_bounds__(256) void k_scan_r(const fvec4* __restrict__ x, fve
   }
 }
 
+// the fused rank + bond scan's shape: a 1024-thread block owns all V = 256
+// rows of a 16-miner strip (thread = 1 row x 4 miners, a wave = 16 rows x
+// 64 B); per step a column sum over the rows (wave butterfly -> LDS -> one
+// barrier every G steps) models the in-block rank reduction
+template <int P, int G, bool RED>
+__global__ __launch_bounds__(1024) void k_scan16(const fvec4* __restrict__ x, fvec4* __restrict__ y, int steps,
+                                                 int V, int M, float* __restrict__ out) {
+  __shared__ fvec4 part[G][16][4];
+  const int strips = M / 16;
+  int blk = blockIdx.x;
+  if ((gridDim.x & 7) == 0) blk = (blk & 7) * (gridDim.x >> 3) + (blk >> 3);  // neighbours share an XCD
+  const int strip = blk % strips;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, q = lane & 3;
+  const int row = wave * 16 + (lane >> 2);
+  const long long m4 = (long long)M / 4;
+  const long long off = (long long)row * m4 + strip * 4 + q;
+  const long long sl = (long long)V * m4;
+  fvec4 ring[P];
+  fvec4 acc = {0.f, 0.f, 0.f, 0.f}, tot = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int k = 0; k < P; ++k) ring[k] = x[k * sl + off];
+  for (int t0 = 0; t0 < steps; t0 += G) {
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const int t = t0 + g;
+      const int k = g % P;
+      acc = acc * 0.5f + ring[k];
+      __builtin_nontemporal_store(acc, y + t * sl + off);
+      if (t + P < steps) ring[k] = x[(t + P) * sl + off];
+      if (RED) {
+        fvec4 r = acc;
+#pragma unroll
+        for (int o = 4; o < 64; o <<= 1) {
+          r.x += __shfl_xor(r.x, o, 64);
+          r.y += __shfl_xor(r.y, o, 64);
+          r.z += __shfl_xor(r.z, o, 64);
+          r.w += __shfl_xor(r.w, o, 64);
+        }
+        if (lane < 4) part[g][wave][q] = r;
+      }
+    }
+    if (RED) {
+      __syncthreads();
+      if (lane < 16 && wave < G) {
+        float s = 0.f;
+        for (int w = 0; w < 16; ++w) s += part[wave][w][lane >> 2][lane & 3];
+        tot.x += s;
+      }
+      __syncthreads();
+    }
+  }
+  if (tot.x == 1234.5f) out[0] = tot.x;
+}
+
 template <typename F>
 static float time_ms(int reps, F f) {
   hipEvent_t a, b;
@@ -198,6 +252,10 @@ int main() {
     rep("scan R2 P4 nt", 2 * B * 1000 / 1024, time_ms(reps, [&] { hipLaunchKernelGGL((k_scan_r<4, 2, true>), dim3(g / 2), dim3(256), 0, 0, x, y, steps, V, M); }));
     rep("scan R2 P8 nt", 2 * B * 1000 / 1024, time_ms(reps, [&] { hipLaunchKernelGGL((k_scan_r<8, 2, true>), dim3(g / 2), dim3(256), 0, 0, x, y, steps, V, M); }));
     rep("scan R4 P4 nt", 2 * B * 1000 / 1024, time_ms(reps, [&] { hipLaunchKernelGGL((k_scan_r<4, 4, true>), dim3(g / 4), dim3(256), 0, 0, x, y, steps, V, M); }));
+    rep("scan16 P4 (strip, no reduce)", 2 * B * 1000 / 1024, time_ms(reps, [&] { hipLaunchKernelGGL((k_scan16<4, 4, false>), dim3(M / 16), dim3(1024), 0, 0, x, y, steps, V, M, out); }));
+    rep("scan16 P4 G8 reduce", 2 * B * 1000 / 1024, time_ms(reps, [&] { hipLaunchKernelGGL((k_scan16<4, 8, true>), dim3(M / 16), dim3(1024), 0, 0, x, y, steps, V, M, out); }));
+    rep("scan16 P2 G8 reduce", 2 * B * 1000 / 1024, time_ms(reps, [&] { hipLaunchKernelGGL((k_scan16<2, 8, true>), dim3(M / 16), dim3(1024), 0, 0, x, y, steps, V, M, out); }));
+    rep("scan16 P8 G8 reduce", 2 * B * 1000 / 1024, time_ms(reps, [&] { hipLaunchKernelGGL((k_scan16<8, 8, true>), dim3(M / 16), dim3(1024), 0, 0, x, y, steps, V, M, out); }));
     rep("scan R1 P8", 2 * B * 1000 / 1024, time_ms(reps, [&] { hipLaunchKernelGGL((k_scan_r<8, 1, false>), dim3(g), dim3(256), 0, 0, x, y, steps, V, M); }));
   }
   return 0;
