@@ -420,8 +420,12 @@ def bench_wide(args, world: int, rank: int, dist: bool) -> dict:
         def step():
             return wide.run_wide_distributed(variant, params, W, S, M_total=M, want_hist=hist)
     else:
+        # one GPU holds the whole subnet: the unsharded engine (one yuma_run),
+        # no shard stages or exchanges
+        ws = torch.empty(engine.workspace_bytes(variant, 1, E, V, M, False), dtype=torch.uint8, device=dev)
+
         def step():
-            return wide.run_wide_local(variant, params, W, S, 1, want_hist=hist)
+            return engine.run(variant, params, W, S, want_hist=hist, workspace=ws)
 
     elapsed = timed(step, args.warmup, args.steps, dist, dev)
     value = float(E) * args.steps / elapsed  # one subnet: total work fixed
@@ -429,7 +433,8 @@ def bench_wide(args, world: int, rank: int, dist: bool) -> dict:
     workload = {"workload": f"c4: wide subnet {V}V x {M}M x {E} epochs, {args.version}, miner columns "
                             f"sharded x{world}", "V": V, "M": M, "epochs": E, "scenarios_per_gpu": 1,
                 "version": args.version, "bond_history": hist,
-                "parallelism": f"miner-column sharded x{world} (all-gather of per-shard partials)"}
+                "parallelism": (f"miner-column sharded x{world} (all-gather of per-shard partials)" if dist
+                                else "single GPU, unsharded engine")}
     line = base_line(args, world, value, "scenario-epochs/s", elapsed, "strong", workload)
     pmc = load_traffic({k: workload[k] for k in ("V", "M", "epochs", "scenarios_per_gpu", "version",
                                                   "bond_history")}) if world == 1 else None
