@@ -162,8 +162,12 @@ def cpu_baseline(variant: str, W_dev, S_dev, cfgs: list, seconds: float, warmup:
     torch.set_num_threads(host["threads"])
     n_sc = len(cfgs)
     ring = min(ring, W_dev.shape[0])
-    W = W_dev[:ring, :n_sc].cpu()
-    S = S_dev[:ring, :n_sc].cpu()
+    if W_dev.shape[1] == 1 and n_sc > 1:  # one shared trajectory (the c3 sweep)
+        W = W_dev[:ring, :1].cpu().expand(-1, n_sc, -1, -1)
+        S = S_dev[:ring, :1].cpu().expand(-1, n_sc, -1)
+    else:
+        W = W_dev[:ring, :n_sc].cpu()
+        S = S_dev[:ring, :n_sc].cpu()
 
     def rate(mode: str, n_warm: int, max_epochs: int, budget: float) -> tuple[float, int, float]:
         B = [None] * n_sc
@@ -261,14 +265,16 @@ def sweep_config(g: int):
                                              alpha_low=lo, alpha_high=hi))
 
 
-def engine_line(args, variant: int, params: list, W, S, world: int, dist: bool, workload: dict) -> dict:
+def engine_line(args, variant: int, params: list, W, S, world: int, dist: bool, workload: dict,
+                shared: bool = False) -> dict:
     """Time one engine configuration on resident inputs and build its line:
     the step (graph replay of the whole E-epoch run), per-phase HIP-event
     device time, the §8d step roofline and the dominant kernel's roofline."""
     from yuma_simulation._internal import engine
 
     dev = W.device
-    E, N, V, M = W.shape
+    E, _, V, M = W.shape
+    N = len(params)
     liquid = any(p.liquid_mode != engine.LIQUID_OFF for p in params)
     hist = not args.no_history
     out = {"Dn": torch.empty(E, N, V, device=dev), "C": torch.empty(E, N, M, device=dev),
@@ -280,11 +286,13 @@ def engine_line(args, variant: int, params: list, W, S, world: int, dist: bool, 
     graph = None
     if args.no_graph:
         def step():
-            return engine.run(variant, params, W, S, want_hist=hist, out=out, workspace=ws, chunk_epochs=chunk)
+            return engine.run(variant, params, W, S, want_hist=hist, out=out, workspace=ws, chunk_epochs=chunk,
+                              shared_inputs=shared)
     else:
         # the whole E-epoch run captured once into a HIP graph (yuma_graph_create);
         # each timed step is one replay of it over the same resident inputs
-        graph = engine.RunGraph(variant, params, W, S, want_hist=hist, out=out, workspace=ws, chunk_epochs=chunk)
+        graph = engine.RunGraph(variant, params, W, S, want_hist=hist, out=out, workspace=ws, chunk_epochs=chunk,
+                                shared_inputs=shared)
         step = graph.launch
 
     elapsed = timed(step, args.warmup, args.steps, dist, dev)
@@ -296,7 +304,8 @@ def engine_line(args, variant: int, params: list, W, S, world: int, dist: bool, 
     phases = np.zeros(len(engine.PHASES))
     for _ in range(args.profile_reps):
         buf = [0.0] * len(engine.PHASES)
-        engine.run(variant, params, W, S, want_hist=hist, out=out, workspace=ws, chunk_epochs=chunk, phase_ms=buf)
+        engine.run(variant, params, W, S, want_hist=hist, out=out, workspace=ws, chunk_epochs=chunk, phase_ms=buf,
+                   shared_inputs=shared)
         phases += np.array(buf)
     phases /= args.profile_reps
     if graph is not None:
@@ -345,6 +354,9 @@ def engine_line(args, variant: int, params: list, W, S, world: int, dist: bool, 
             "timing": "HIP events on the launch stream around the kernel (yuma_run_profiled)",
         },
     }
+    if shared:
+        line["roofline"]["note"] = ("every scenario reads one shared W/S trajectory: beyond the epoch-step "
+                                    "contract (SURVEY 8d), so frac counts the contract bytes per scenario-epoch")
     line["phases"] = phase_info
     return line
 
@@ -368,21 +380,24 @@ def bench_engine(args, world: int, rank: int, dist: bool) -> dict:
     hist = not args.no_history
     seed = args.seed + 7919 * rank  # each rank simulates its own subnet(s)
 
-    # inputs resident in HBM before timing
-    W = engine.synth_weights(seed, E, N, V, M)
-    S = torch.from_numpy(synth.stakes(seed, E, N, V)).to(dev)
+    # inputs resident in HBM before timing; the c3 sweep runs every scenario
+    # over ONE subnet trajectory (shared W/S, params vary)
+    shared = args.config == "c3"
+    Nin = 1 if shared else N
+    W = engine.synth_weights(seed, E, Nin, V, M)
+    S = torch.from_numpy(synth.stakes(seed, E, Nin, V)).to(dev)
 
     def workload_of(version: str, liq: bool) -> dict:
         if args.config == "c3":
             wl = (f"c3: parameter sweep, {N} scenarios per GPU (of the 4096-point bond_alpha x kappa x "
-                  f"liquid x alpha grid) of {V}V x {M}M x {E} epochs, {version}")
+                  f"liquid x alpha grid) over one shared {V}V x {M}M x {E}-epoch subnet trajectory, {version}")
         else:
             wl = f"c2: single subnet {V}V x {M}M x {E} epochs, {version}" + (" (liquid)" if liq else "")
         return {"workload": wl, "V": V, "M": M, "epochs": E, "scenarios_per_gpu": N, "version": version,
                 "bond_history": hist, "launch": "direct" if args.no_graph else "hipGraph replay",
                 "parallelism": f"scenario-sharded x{world}" if world > 1 else "single GPU"}
 
-    line = engine_line(args, variant, params, W, S, world, dist, workload_of(args.version, liquid))
+    line = engine_line(args, variant, params, W, S, world, dist, workload_of(args.version, liquid), shared=shared)
     if args.config == "c2" and not args.no_also:
         # SURVEY §7 "Config 2 naming": c2 is quoted for Yuma 3 AND Yuma 4 liquid
         v4 = "Yuma 4 (Rhef+relative bonds) - liquid alpha on"

@@ -152,6 +152,18 @@ int yuma_run(int variant, const yuma_params_t* params_dev, int N, int E, int V, 
              const yuma_outputs_t* out, void* workspace, size_t workspace_bytes,
              int chunk_epochs, void* stream);
 
+/* yuma_run with options. flags: YUMA_RUN_SHARED_INPUTS — every scenario reads
+ * the same input trajectory: W is [E][V][M] and S [E][V] (a parameter sweep
+ * over one subnet; SURVEY config c3), so a whole sweep moves one copy of W
+ * per epoch through HBM and the scenarios' reads of it meet in the caches.
+ * Results are those of yuma_run on W and S replicated per scenario.
+ * phase_ms: NULL, or per-phase device time as yuma_run_profiled (blocks).   */
+enum yuma_run_flags { YUMA_RUN_SHARED_INPUTS = 1 };
+int yuma_run_ex(int variant, const yuma_params_t* params_dev, int N, int E, int V, int M,
+                const float* W, const float* S, const float* B_init, const float* Wprev_init,
+                const yuma_outputs_t* out, void* workspace, size_t workspace_bytes,
+                int chunk_epochs, int flags, void* stream, float* phase_ms);
+
 /* hipGraph form of yuma_run: the whole multi-epoch run (every phase of every
  * chunk, no host work between them) captured once into a HIP graph and
  * replayed with one hipGraphLaunch. The arguments are those of yuma_run and
@@ -166,6 +178,11 @@ int yuma_graph_create(yuma_graph_t* graph, int variant, const yuma_params_t* par
                       int E, int V, int M, const float* W, const float* S,
                       const float* B_init, const float* Wprev_init, const yuma_outputs_t* out,
                       void* workspace, size_t workspace_bytes, int chunk_epochs);
+/* yuma_graph_create with yuma_run_ex's flags. */
+int yuma_graph_create_ex(yuma_graph_t* graph, int variant, const yuma_params_t* params_dev, int N,
+                         int E, int V, int M, const float* W, const float* S,
+                         const float* B_init, const float* Wprev_init, const yuma_outputs_t* out,
+                         void* workspace, size_t workspace_bytes, int chunk_epochs, int flags);
 /* Replay on `stream` (stream-ordered, no host synchronisation). */
 int yuma_graph_launch(yuma_graph_t graph, void* stream);
 /* Kernel nodes in the captured graph (diagnostics / tests). */

@@ -125,6 +125,27 @@ __device__ __forceinline__ float div_rn(float a, const RowDiv& rd) {
   return slow ? a / rd.d : q;
 }
 
+// Input slice of a slice (epoch t, scenario n) = t N + n: the slice itself,
+// or epoch t when every scenario reads the same input trajectory (wsh: a
+// parameter sweep over one subnet, yuma_run_shared).
+__device__ __forceinline__ long long in_slice(long long slice, int N, int wsh) {
+  return wsh ? slice / N : slice;
+}
+
+// Block -> (slice, sub-block): slice-major; with shared inputs
+// scenario-minor, so the N scenarios' blocks over the same rows / tile of an
+// input slice are consecutive and their reads of it meet in the caches.
+struct SliceBlock {
+  long long slice;
+  int sub;
+};
+__device__ __forceinline__ SliceBlock slice_block(long long slice0, int subs, int N, int wsh) {
+  const long long b = blockIdx.x;
+  if (!wsh) return {slice0 + b / subs, (int)(b % subs)};
+  const long long n = b % N, r = b / N;
+  return {slice0 + (r / subs) * N + n, (int)(r % subs)};
+}
+
 // thread -> (row group g, column quad c4). A wave covers 4 row groups x 64
 // columns, so one float4 load instruction moves 4 x 256 contiguous bytes.
 struct Lay {
@@ -301,13 +322,16 @@ __global__ __launch_bounds__(256) void k_rowsum(const float* __restrict__ W,
                                                 const float* __restrict__ S, int V, int M,
                                                 long long slice0, int rowblocks,
                                                 float* __restrict__ rsd, float* __restrict__ sn,
-                                                int partial, int* __restrict__ sx) {
+                                                int partial, int* __restrict__ sx, int N,
+                                                int wsh) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const long long slice = slice0 + blockIdx.x / rowblocks;
-  const int rb = blockIdx.x % rowblocks;
+  const SliceBlock sb = slice_block(slice0, rowblocks, N, wsh);
+  const long long slice = sb.slice;
+  const long long wsl = in_slice(slice, N, wsh);
+  const int rb = sb.sub;
   const int row = rb * 4 + wave;
   if (row < V) {
-    const float* r = W + (slice * V + row) * (long long)M;
+    const float* r = W + (wsl * V + row) * (long long)M;
     float acc = 0.0f;
     for (int m0 = 0; m0 < M; m0 += 256) {
       const int m = m0 + lane * 4;
@@ -334,7 +358,7 @@ __global__ __launch_bounds__(256) void k_rowsum(const float* __restrict__ W,
     if (lane == 0) rsd[slice * V + row] = partial ? acc : acc + 1e-6f;
   }
   if (rb == 0 && wave == 0) {
-    const float* s = S + slice * V;
+    const float* s = S + wsl * V;
     float acc = 0.0f;
     for (int v = lane; v < V; v += 64) acc = acc + s[v];
     acc = wave_sum(acc);
@@ -370,7 +394,7 @@ __global__ __launch_bounds__(NT) void k_consensus(const float* __restrict__ W,
                                                   const yuma_params_t* __restrict__ prm, int N,
                                                   int V, int M, long long slice0, int tiles,
                                                   double* __restrict__ craw,
-                                                  float* __restrict__ Pout) {
+                                                  float* __restrict__ Pout, int wsh) {
   constexpr int NW = NT / 64, G = NT / 16;
   __shared__ float4 red[2][NW * 16];
   const Lay L = lay();
@@ -378,7 +402,7 @@ __global__ __launch_bounds__(NT) void k_consensus(const float* __restrict__ W,
   const int tile = blockIdx.x % tiles;
   const int n = (int)(slice % N);
   const int m = tile * kTileM + L.c4 * 4;
-  const float* Ws = W + slice * (long long)V * M;
+  const float* Ws = W + in_slice(slice, N, wsh) * (long long)V * M;
 
   float wn[R][4], s[R], d[R];
 #pragma unroll
@@ -982,17 +1006,18 @@ __global__ __launch_bounds__(256, 3) void k_consensus_w(const float* __restrict_
                                                      const yuma_params_t* __restrict__ prm, int N,
                                                      int V, int M, long long slice0, int tiles,
                                                      double* __restrict__ craw,
-                                                     float* __restrict__ Pout) {
+                                                     float* __restrict__ Pout, int wsh) {
   __shared__ __attribute__((aligned(16))) unsigned hb[kHistWords];
   const WLay L = wlay();
-  const long long slice = slice0 + blockIdx.x / tiles;
-  const int tile = blockIdx.x % tiles;
+  const SliceBlock sb = slice_block(slice0, tiles, N, wsh);
+  const long long slice = sb.slice;
+  const int tile = sb.sub;
   const int n = (int)(slice % N);
   const int m = tile * kTileM + L.wave * 16 + L.cq * 4;
   if (tile * kTileM + L.wave * 16 >= M) return;  // whole wave past the last miner
   float wn[R][4], s[R];
-  load_norm_w<R, VEC, false>(W + slice * (long long)V * M, rsd + slice * V, sn + slice * V, V, M,
-                             m, L.rg, wn, s);
+  load_norm_w<R, VEC, false>(W + in_slice(slice, N, wsh) * (long long)V * M, rsd + slice * V,
+                             sn + slice * V, V, M, m, L.rg, wn, s);
   if (Pout != nullptr) prerank_store<R>(wn, s, L, m, M, Pout + slice * M);
   int hi_k[4];
   const yuma_params_t& p = prm[n];
@@ -1014,7 +1039,7 @@ __global__ __launch_bounds__(256) void k_rank_w(
     const float* __restrict__ C, const float* __restrict__ Wprev_init, int yuma2_unused, int N, int V,
     int M, long long slice0, int tiles, float* __restrict__ Rout, float* __restrict__ rpart,
     float* __restrict__ Wn_out, float* __restrict__ Wc_out, float* __restrict__ tvc,
-    float* __restrict__ tvn) {
+    float* __restrict__ tvn, int wsh) {
   __shared__ float wsums[4];
   const WLay L = wlay();
   const long long slice = slice0 + blockIdx.x / tiles;
@@ -1024,7 +1049,8 @@ __global__ __launch_bounds__(256) void k_rank_w(
   const long long VM = (long long)V * M;
   const int m = tile * kTileM + L.wave * 16 + L.cq * 4;
   float wn[R][4], s[R];
-  load_norm_w<R, VEC>(W + slice * VM, rsd + slice * V, sn + slice * V, V, M, m, L.rg, wn, s);
+  load_norm_w<R, VEC>(W + in_slice(slice, N, wsh) * VM, rsd + slice * V, sn + slice * V, V, M, m, L.rg,
+                      wn, s);
   float Cc[4];
   vec4c(C + slice * M, m, M, Cc);
   float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
@@ -1041,7 +1067,7 @@ __global__ __launch_bounds__(256) void k_rank_w(
           for (int c = 0; c < 4; ++c) src[c] = wn[i][c];
         }
       } else {
-        load4c<VEC>(W + (slice - N) * VM, row, V, m, M, src);
+        load4c<VEC>(W + in_slice(slice - N, N, wsh) * VM, row, V, m, M, src);
         const RowDiv rdp = row_div(rsd[(slice - N) * V + min(row, V - 1)]);
 #pragma unroll
         for (int c = 0; c < 4; ++c) src[c] = div_rn(src[c], rdp);
@@ -1135,14 +1161,15 @@ __global__ __launch_bounds__(256) void k_rank_s(const float* __restrict__ W,
                                                 const float* __restrict__ C, int N, int V, int M,
                                                 long long slice0, int tiles,
                                                 float* __restrict__ Rout,
-                                                float* __restrict__ rpart) {
+                                                float* __restrict__ rpart, int wsh) {
   __shared__ float4 red[4][16];
   const Lay L = lay();
-  const long long slice = slice0 + blockIdx.x / tiles;
-  const int tile = blockIdx.x % tiles;
+  const SliceBlock sb = slice_block(slice0, tiles, N, wsh);
+  const long long slice = sb.slice;
+  const int tile = sb.sub;
   const long long VM = (long long)V * M;
   const int m = tile * kTileM + L.c4 * 4;
-  const float* Ws = W + slice * VM;
+  const float* Ws = W + in_slice(slice, N, wsh) * VM;
   float Cc[4];
   load4c<VEC>(C + slice * M, 0, 1, m, M, Cc);
   float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
@@ -1396,7 +1423,7 @@ __global__ __launch_bounds__(NT) void k_rank(
     const float* __restrict__ C, const float* __restrict__ Wprev_init, int yuma2, int N, int V,
     int M, long long slice0, int tiles, float* __restrict__ Rout, float* __restrict__ rpart,
     float* __restrict__ Wn_out, float* __restrict__ Wc_out, float* __restrict__ tvc,
-    float* __restrict__ tvn) {
+    float* __restrict__ tvn, int wsh) {
   constexpr int NW = NT / 64, G = NT / 16;
   __shared__ float4 red[NW * 16];
   const Lay L = lay();
@@ -1406,7 +1433,7 @@ __global__ __launch_bounds__(NT) void k_rank(
   const long long t = slice / N;
   const int m = tile * kTileM + L.c4 * 4;
   const long long VM = (long long)V * M;
-  const float* Ws = W + slice * VM;
+  const float* Ws = W + in_slice(slice, N, wsh) * VM;
   float Cc[4];
   load4_vec(C + slice * M, m, M, Cc);
 
@@ -1438,7 +1465,7 @@ __global__ __launch_bounds__(NT) void k_rank(
         }
       } else {
         float xp[4];
-        load4<VEC>(W + (slice - N) * VM + (long long)row * M, m, M, xp);
+        load4<VEC>(W + in_slice(slice - N, N, wsh) * VM + (long long)row * M, m, M, xp);
         const RowDiv rdp = row_div(rsd[(slice - N) * V + row]);
 #pragma unroll
         for (int c = 0; c < 4; ++c) src[c] = div_rn(xp[c], rdp);
@@ -1595,9 +1622,8 @@ struct BondArgs {
   float* Wb_out;
   float* Binst_out;
   float* dpart;
-  float* R;      // k_bonds_rank: server_rank [slice][M]
-  float* rpart;  // k_bonds_rank: per-strip rank sums [slice][tiles]
   int N, V, M, tiles, rowblocks, t0, t1;
+  int wsh;  // every scenario reads input slice t (yuma_run_shared)
 };
 
 template <int VARIANT, int NT, int R, bool VEC>
@@ -1660,12 +1686,13 @@ __global__ __launch_bounds__(NT) void k_bonds(BondArgs A) {
     } else {
       have_wp = true;
       const long long ps = (long long)(A.t0 - 1) * N + n;
+      const long long pw = A.wsh ? (long long)(A.t0 - 1) : ps;
 #pragma unroll
       for (int i = 0; i < R; ++i) {
         const int row = row0 + G * i;
         if (row < V) {
           float x[4];
-          load4<VEC>(A.W + ps * VM + (long long)row * M, m, M, x);
+          load4<VEC>(A.W + pw * VM + (long long)row * M, m, M, x);
           const float d = A.rsd[ps * V + row];
 #pragma unroll
           for (int c = 0; c < 4; ++c) Wp[i][c] = x[c] / d;
@@ -1713,8 +1740,9 @@ __global__ __launch_bounds__(NT) void k_bonds(BondArgs A) {
     }
 
     float wn[R][4], s[R], dd[R];
+    const long long wsl = A.wsh ? (long long)t : slice;
 #pragma unroll
-    for (int i = 0; i < R; ++i) load4c<VEC>(A.W + slice * VM, row0 + G * i, V, m, M, wn[i]);
+    for (int i = 0; i < R; ++i) load4c<VEC>(A.W + wsl * VM, row0 + G * i, V, m, M, wn[i]);
 #pragma unroll
     for (int i = 0; i < R; ++i) {
       const int rr = min(row0 + G * i, V - 1);
@@ -1732,7 +1760,7 @@ __global__ __launch_bounds__(NT) void k_bonds(BondArgs A) {
       if (__syncthreads_or(slow)) {
 #pragma unroll
         for (int i = 0; i < R; ++i) {
-          load4c<VEC>(A.W + slice * VM, row0 + G * i, V, m, M, wn[i]);
+          load4c<VEC>(A.W + wsl * VM, row0 + G * i, V, m, M, wn[i]);
 #pragma unroll
           for (int c = 0; c < 4; ++c) wn[i][c] = wn[i][c] / dd[i];
         }
@@ -1873,9 +1901,12 @@ template <int VARIANT, int R, bool VEC, int P, bool VECI, bool NT = false>
 __global__ __launch_bounds__(256) void k_bonds_elem(BondArgs A) {
   constexpr int G = 16;
   const Lay L = lay();
-  const int tile = blockIdx.x % A.tiles;
-  const int rb = (blockIdx.x / A.tiles) % A.rowblocks;
-  const int n = blockIdx.x / (A.tiles * A.rowblocks);
+  // scenario-minor with shared inputs (slice_block): the scenarios walking one
+  // bond tile read the same W tile at the same epochs
+  const int bx = A.wsh ? (int)(blockIdx.x / A.N) : (int)blockIdx.x;
+  const int tile = bx % A.tiles;
+  const int rb = (bx / A.tiles) % A.rowblocks;
+  const int n = A.wsh ? (int)(blockIdx.x % A.N) : (int)(blockIdx.x / (A.tiles * A.rowblocks));
   const int N = A.N, V = A.V, M = A.M;
   const long long VM = (long long)V * M;
   const int m = tile * kTileM + L.c4 * 4;
@@ -1911,7 +1942,7 @@ __global__ __launch_bounds__(256) void k_bonds_elem(BondArgs A) {
 #pragma unroll
     for (int i = 0; i < R; ++i) {
       const int rr = min(row0 + G * i, V - 1);
-      load4c<VEC>(A.W + slice * VM, rr, V, m, M, rw[k][i]);
+      load4c<VEC>(A.W + (A.wsh ? (long long)t : slice) * VM, rr, V, m, M, rw[k][i]);
       rd[k][i] = A.rsd[slice * V + rr];
       rsn[k][i] = A.sn[slice * V + rr];
     }
@@ -2257,28 +2288,28 @@ RowCfg row_cfg(int V) {
 template <int R, bool VEC>
 void launch_consensus_w(long long nblocks, hipStream_t st, const float* W, const float* rsd,
                         const float* sn, const int* sx, const yuma_params_t* prm, int N, int V,
-                        int M, long long slice0, int tiles, double* craw, float* P) {
+                        int M, long long slice0, int tiles, double* craw, float* P, int wsh) {
   YK_LAUNCH((yk::k_consensus_w<R, VEC>), nblocks, 256, st, W, rsd, sn, sx, prm, N, V, M, slice0,
-            tiles, craw, P);
+            tiles, craw, P, wsh);
 }
 
 template <bool VEC>
 void launch_consensus(RowCfg rc, long long nblocks, hipStream_t st, const float* W,
                       const float* rsd, const float* sn, const int* sx,
                       const yuma_params_t* prm, int N, int V, int M, long long slice0, int tiles,
-                      double* craw, float* P) {
+                      double* craw, float* P, int wsh) {
   switch (rc) {  // wave-owned columns up to 256 validators
     case RC_256_1:
       launch_consensus_w<1, VEC>(nblocks, st, W, rsd, sn, sx, prm, N, V, M, slice0, tiles, craw,
-                                  P);
+                                  P, wsh);
       return;
     case RC_256_4:
       launch_consensus_w<4, VEC>(nblocks, st, W, rsd, sn, sx, prm, N, V, M, slice0, tiles, craw,
-                                  P);
+                                  P, wsh);
       return;
     case RC_256_16:
       launch_consensus_w<16, VEC>(nblocks, st, W, rsd, sn, sx, prm, N, V, M, slice0, tiles, craw,
-                                  P);
+                                  P, wsh);
       return;
     default:
       break;
@@ -2286,19 +2317,19 @@ void launch_consensus(RowCfg rc, long long nblocks, hipStream_t st, const float*
   switch (rc) {
     case RC_256_1:
       YK_LAUNCH((yk::k_consensus<256, 1, VEC>), nblocks, 256, st, W, rsd, sn, prm, N, V, M,
-                slice0, tiles, craw, P);
+                slice0, tiles, craw, P, wsh);
       break;
     case RC_256_4:
       YK_LAUNCH((yk::k_consensus<256, 4, VEC>), nblocks, 256, st, W, rsd, sn, prm, N, V, M,
-                slice0, tiles, craw, P);
+                slice0, tiles, craw, P, wsh);
       break;
     case RC_256_16:
       YK_LAUNCH((yk::k_consensus<256, 16, VEC>), nblocks, 256, st, W, rsd, sn, prm, N, V, M,
-                slice0, tiles, craw, P);
+                slice0, tiles, craw, P, wsh);
       break;
     case RC_1024_16:
       YK_LAUNCH((yk::k_consensus<1024, 16, VEC>), nblocks, 1024, st, W, rsd, sn, prm, N, V, M,
-                slice0, tiles, craw, P);
+                slice0, tiles, craw, P, wsh);
       break;
   }
 }
@@ -2307,15 +2338,15 @@ template <bool VEC>
 void launch_rank(RowCfg rc, long long nblocks, hipStream_t st, const float* W, const float* rsd,
                  const float* sn, const float* C, const float* Wprev_init, int yuma2, int N,
                  int V, int M, long long slice0, int tiles, float* R, float* rpart, float* Wn,
-                 float* Wc, float* tvc, float* tvn) {
+                 float* Wc, float* tvc, float* tvn, int wsh) {
   const bool full = Wn != nullptr || Wc != nullptr || tvc != nullptr;
   if (!full && !yuma2) {  // streaming rank; k_rank_w also materialises Wn / Wc / T_v or clips W_prev
-    YK_LAUNCH(yk::k_rank_s<VEC>, nblocks, 256, st, W, rsd, sn, C, N, V, M, slice0, tiles, R, rpart);
+    YK_LAUNCH(yk::k_rank_s<VEC>, nblocks, 256, st, W, rsd, sn, C, N, V, M, slice0, tiles, R, rpart, wsh);
     return;
   }
   auto go = [&](auto kern) {
     YK_LAUNCH(kern, nblocks, 256, st, W, rsd, sn, C, Wprev_init, yuma2, N, V, M, slice0, tiles, R,
-              rpart, Wn, Wc, tvc, tvn);
+              rpart, Wn, Wc, tvc, tvn, wsh);
   };
 #define YK_RANKW(RR)                                                   \
   if (yuma2) {                                                         \
@@ -2339,19 +2370,19 @@ void launch_rank(RowCfg rc, long long nblocks, hipStream_t st, const float* W, c
   switch (rc) {
     case RC_256_1:
       YK_LAUNCH((yk::k_rank<256, 1, VEC>), nblocks, 256, st, W, rsd, sn, C, Wprev_init, yuma2,
-                N, V, M, slice0, tiles, R, rpart, Wn, Wc, tvc, tvn);
+                N, V, M, slice0, tiles, R, rpart, Wn, Wc, tvc, tvn, wsh);
       break;
     case RC_256_4:
       YK_LAUNCH((yk::k_rank<256, 4, VEC>), nblocks, 256, st, W, rsd, sn, C, Wprev_init, yuma2,
-                N, V, M, slice0, tiles, R, rpart, Wn, Wc, tvc, tvn);
+                N, V, M, slice0, tiles, R, rpart, Wn, Wc, tvc, tvn, wsh);
       break;
     case RC_256_16:
       YK_LAUNCH((yk::k_rank<256, 16, VEC>), nblocks, 256, st, W, rsd, sn, C, Wprev_init, yuma2,
-                N, V, M, slice0, tiles, R, rpart, Wn, Wc, tvc, tvn);
+                N, V, M, slice0, tiles, R, rpart, Wn, Wc, tvc, tvn, wsh);
       break;
     case RC_1024_16:
       YK_LAUNCH((yk::k_rank<1024, 16, VEC>), nblocks, 1024, st, W, rsd, sn, C, Wprev_init,
-                yuma2, N, V, M, slice0, tiles, R, rpart, Wn, Wc, tvc, tvn);
+                yuma2, N, V, M, slice0, tiles, R, rpart, Wn, Wc, tvc, tvn, wsh);
       break;
   }
 }
@@ -2437,7 +2468,7 @@ struct PhaseTimer {
 int run_impl(int variant, const yuma_params_t* prm, int N, int E, int V, int M, const float* W,
              const float* S, const float* B_init, const float* Wprev_init,
              const yuma_outputs_t* out, void* workspace, size_t ws_bytes, int chunk,
-             void* stream, float* phase_ms = nullptr) {
+             void* stream, float* phase_ms = nullptr, int wsh = 0) {
   if (variant < 0 || variant > 4) return fail(YUMA_EINVAL, "unknown variant %d", variant);
   if (N < 1 || E < 1 || V < 1 || M < 1)
     return fail(YUMA_EINVAL, "sizes must be positive (N=%d E=%d V=%d M=%d)", N, E, V, M);
@@ -2492,17 +2523,17 @@ int run_impl(int variant, const yuma_params_t* prm, int N, int E, int V, int M, 
       tm.mark(YUMA_PHASE_ROWSUM);
       if (vec)
         YK_LAUNCH(yk::k_rowsum<true>, ns * rowblocks4, 256, st, W, S, V, M, s0, rowblocks4,
-                  ws.rsd, ws.sn, 0, ws.sx);
+                  ws.rsd, ws.sn, 0, ws.sx, N, wsh);
       else
         YK_LAUNCH(yk::k_rowsum<false>, ns * rowblocks4, 256, st, W, S, V, M, s0, rowblocks4,
-                  ws.rsd, ws.sn, 0, ws.sx);
+                  ws.rsd, ws.sn, 0, ws.sx, N, wsh);
       tm.mark(YUMA_PHASE_CONSENSUS);
       if (vec)
         launch_consensus<true>(rc, ns * tiles, st, W, ws.rsd, ws.sn, ws.sx, prm, N, V, M, s0, tiles,
-                               ws.craw, out->P);
+                               ws.craw, out->P, wsh);
       else
         launch_consensus<false>(rc, ns * tiles, st, W, ws.rsd, ws.sn, ws.sx, prm, N, V, M, s0,
-                                tiles, ws.craw, out->P);
+                                tiles, ws.craw, out->P, wsh);
       tm.mark(YUMA_PHASE_QUANTISE);
       YK_LAUNCH(yk::k_quantise<256>, ns, 256, st, ws.craw, prm, variant, N, M, s0, C, ws.qlev,
                 ba_buf, ws.scal, nullptr, nullptr, 0);
@@ -2510,11 +2541,11 @@ int run_impl(int variant, const yuma_params_t* prm, int N, int E, int V, int M, 
       if (vec)
         launch_rank<true>(rc, ns * tiles, st, W, ws.rsd, ws.sn, C, Wprev_init,
                           variant == YUMA_VARIANT_YUMA2, N, V, M, s0, tiles, Rr, ws.rpart, out->Wn,
-                          out->Wc, ws.tvc, ws.tvn);
+                          out->Wc, ws.tvc, ws.tvn, wsh);
       else
         launch_rank<false>(rc, ns * tiles, st, W, ws.rsd, ws.sn, C, Wprev_init,
                            variant == YUMA_VARIANT_YUMA2, N, V, M, s0, tiles, Rr, ws.rpart,
-                           out->Wn, out->Wc, ws.tvc, ws.tvn);
+                           out->Wn, out->Wc, ws.tvc, ws.tvn, wsh);
     }
     tm.mark(YUMA_PHASE_INCENTIVE);
     YK_LAUNCH(yk::k_incentive, ns, 256, st, Rr, ws.rpart, out->P, M, s0, tiles, I,
@@ -2542,6 +2573,7 @@ int run_impl(int variant, const yuma_params_t* prm, int N, int E, int V, int M, 
     A.rowblocks = rowblocks;
     A.t0 = c0;
     A.t1 = c1;
+    A.wsh = wsh;
     const long long nb = (long long)N * tiles * rowblocks;
     tm.mark(YUMA_PHASE_BONDS);
     if (vec)
@@ -2623,10 +2655,10 @@ int shard_stage_impl(int stage, int variant, const yuma_params_t* prm, int N, in
       const int rb4 = (V + 3) / 4;
       if (vec)
         YK_LAUNCH(yk::k_rowsum<true>, ns * rb4, 256, st, W, S, V, M, 0LL, rb4, io->rowsum_part,
-                  ws.sn, 1, ws.sx);
+                  ws.sn, 1, ws.sx, N, 0);
       else
         YK_LAUNCH(yk::k_rowsum<false>, ns * rb4, 256, st, W, S, V, M, 0LL, rb4, io->rowsum_part,
-                  ws.sn, 1, ws.sx);
+                  ws.sn, 1, ws.sx, N, 0);
       break;
     }
     case 2: {
@@ -2637,10 +2669,10 @@ int shard_stage_impl(int stage, int variant, const yuma_params_t* prm, int N, in
       YK_LAUNCH(yk::k_add_eps, nb, 256, st, io->rowsum, ns * V, ws.rsd);
       if (vec)
         launch_consensus<true>(rc, ns * tiles, st, W, ws.rsd, ws.sn, ws.sx, prm, N, V, M, 0LL, tiles,
-                               ws.craw, out->P);
+                               ws.craw, out->P, 0);
       else
         launch_consensus<false>(rc, ns * tiles, st, W, ws.rsd, ws.sn, ws.sx, prm, N, V, M, 0LL, tiles,
-                                ws.craw, out->P);
+                                ws.craw, out->P, 0);
       YK_LAUNCH(yk::k_csum, ns, 256, st, ws.craw, rust ? 1 : 0, M, io->csum_part, io->csum_part_d);
       break;
     }
@@ -2652,11 +2684,11 @@ int shard_stage_impl(int stage, int variant, const yuma_params_t* prm, int N, in
       if (vec)
         launch_rank<true>(rc, ns * tiles, st, W, ws.rsd, ws.sn, C, Wprev_init,
                           variant == YUMA_VARIANT_YUMA2, N, V, M, 0LL, tiles, R, ws.rpart,
-                          out->Wn, out->Wc, nullptr, nullptr);
+                          out->Wn, out->Wc, nullptr, nullptr, 0);
       else
         launch_rank<false>(rc, ns * tiles, st, W, ws.rsd, ws.sn, C, Wprev_init,
                            variant == YUMA_VARIANT_YUMA2, N, V, M, 0LL, tiles, R, ws.rpart,
-                           out->Wn, out->Wc, nullptr, nullptr);
+                           out->Wn, out->Wc, nullptr, nullptr, 0);
       YK_LAUNCH(yk::k_rsum, ns, 64, st, ws.rpart, tiles, io->rsum_part);
       break;
     }
@@ -2740,6 +2772,16 @@ int yuma_run(int variant, const yuma_params_t* params_dev, int N, int E, int V, 
                   workspace_bytes, chunk_epochs, stream);
 }
 
+int yuma_run_ex(int variant, const yuma_params_t* params_dev, int N, int E, int V, int M,
+                const float* W, const float* S, const float* B_init, const float* Wprev_init,
+                const yuma_outputs_t* out, void* workspace, size_t workspace_bytes,
+                int chunk_epochs, int flags, void* stream, float* phase_ms) {
+  if (flags & ~YUMA_RUN_SHARED_INPUTS) return fail(YUMA_EINVAL, "unknown run flags 0x%x", flags);
+  return run_impl(variant, params_dev, N, E, V, M, W, S, B_init, Wprev_init, out, workspace,
+                  workspace_bytes, chunk_epochs, stream, phase_ms,
+                  (flags & YUMA_RUN_SHARED_INPUTS) ? 1 : 0);
+}
+
 int yuma_run_profiled(int variant, const yuma_params_t* params_dev, int N, int E, int V, int M,
                       const float* W, const float* S, const float* B_init,
                       const float* Wprev_init, const yuma_outputs_t* out, void* workspace,
@@ -2779,10 +2821,11 @@ int yuma_shard_stage(int stage, int variant, const yuma_params_t* params_dev, in
                           out, workspace, workspace_bytes, stream);
 }
 
-int yuma_graph_create(yuma_graph_t* graph, int variant, const yuma_params_t* params_dev, int N,
-                      int E, int V, int M, const float* W, const float* S,
-                      const float* B_init, const float* Wprev_init, const yuma_outputs_t* out,
-                      void* workspace, size_t workspace_bytes, int chunk_epochs) {
+int yuma_graph_create_ex(yuma_graph_t* graph, int variant, const yuma_params_t* params_dev, int N,
+                         int E, int V, int M, const float* W, const float* S,
+                         const float* B_init, const float* Wprev_init, const yuma_outputs_t* out,
+                         void* workspace, size_t workspace_bytes, int chunk_epochs, int flags) {
+  if (flags & ~YUMA_RUN_SHARED_INPUTS) return fail(YUMA_EINVAL, "unknown run flags 0x%x", flags);
   if (graph == nullptr) return fail(YUMA_EINVAL, "graph handle pointer is NULL");
   *graph = nullptr;
   hipStream_t cs = nullptr;
@@ -2793,7 +2836,8 @@ int yuma_graph_create(yuma_graph_t* graph, int variant, const yuma_params_t* par
     return fail(YUMA_EHIP, "hipStreamBeginCapture failed");
   }
   const int rc = run_impl(variant, params_dev, N, E, V, M, W, S, B_init, Wprev_init, out,
-                          workspace, workspace_bytes, chunk_epochs, cs);
+                          workspace, workspace_bytes, chunk_epochs, cs, nullptr,
+                          (flags & YUMA_RUN_SHARED_INPUTS) ? 1 : 0);
   hipGraph_t g = nullptr;
   const hipError_t ec = hipStreamEndCapture(cs, &g);
   (void)hipStreamDestroy(cs);
@@ -2810,6 +2854,14 @@ int yuma_graph_create(yuma_graph_t* graph, int variant, const yuma_params_t* par
   }
   *graph = new yuma_graph{g, x};
   return YUMA_OK;
+}
+
+int yuma_graph_create(yuma_graph_t* graph, int variant, const yuma_params_t* params_dev, int N,
+                      int E, int V, int M, const float* W, const float* S,
+                      const float* B_init, const float* Wprev_init, const yuma_outputs_t* out,
+                      void* workspace, size_t workspace_bytes, int chunk_epochs) {
+  return yuma_graph_create_ex(graph, variant, params_dev, N, E, V, M, W, S, B_init, Wprev_init, out,
+                              workspace, workspace_bytes, chunk_epochs, 0);
 }
 
 int yuma_graph_launch(yuma_graph_t graph, void* stream) {

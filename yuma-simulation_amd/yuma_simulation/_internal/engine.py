@@ -33,6 +33,7 @@ PHASES = ("rowsum", "consensus", "quantise", "rank", "incentive", "bonds", "fina
 FLAG_NO_HIST = 1  # yuma_params_t.flags: plain bisection instead of the histogram finish
 FLAG_RESET_ALL_COLUMNS = 2  # the reset zeroes every column (reset_bonds_index None)
 RESET_NONE, RESET_ALWAYS, RESET_IF_ZERO_CONSENSUS = range(3)
+RUN_SHARED_INPUTS = 1  # yuma_run_ex flags
 LIQUID_OFF, LIQUID_QUANTILE, LIQUID_CONST_AB = range(3)
 OVR_HIGH, OVR_LOW, OVR_FORCE_Q99 = 1, 2, 4
 
@@ -40,10 +41,12 @@ EXPORTED_SYMBOLS = (
     "yuma_workspace_bytes",
     "yuma_run",
     "yuma_run_profiled",
+    "yuma_run_ex",
     "yuma_epoch",
     "yuma_synth_weights",
     "yuma_shard_stage",
     "yuma_graph_create",
+    "yuma_graph_create_ex",
     "yuma_graph_launch",
     "yuma_graph_nodes",
     "yuma_graph_destroy",
@@ -138,6 +141,8 @@ def load_library(path: str | None = None):
         lib.yuma_run.restype = i32
         lib.yuma_run_profiled.argtypes = lib.yuma_run.argtypes + [ctypes.POINTER(ctypes.c_float)]
         lib.yuma_run_profiled.restype = i32
+        lib.yuma_run_ex.argtypes = lib.yuma_run.argtypes[:-1] + [i32, vp, ctypes.POINTER(ctypes.c_float)]
+        lib.yuma_run_ex.restype = i32
         lib.yuma_epoch.argtypes = [i32, vp, i32, i32, i32, vp, vp, vp, vp, vp, vp, sz, vp]
         lib.yuma_epoch.restype = i32
         lib.yuma_shard_stage.argtypes = [i32, i32, vp, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp,
@@ -148,6 +153,8 @@ def load_library(path: str | None = None):
         lib.yuma_graph_create.argtypes = [ctypes.POINTER(vp), i32, vp, i32, i32, i32, i32, vp, vp,
                                           vp, vp, vp, vp, sz, i32]
         lib.yuma_graph_create.restype = i32
+        lib.yuma_graph_create_ex.argtypes = lib.yuma_graph_create.argtypes + [i32]
+        lib.yuma_graph_create_ex.restype = i32
         lib.yuma_graph_launch.argtypes = [vp, vp]
         lib.yuma_graph_launch.restype = i32
         lib.yuma_graph_nodes.argtypes = [vp]
@@ -334,18 +341,30 @@ def run(variant: int, params: list[YumaParamsC], W: torch.Tensor, S: torch.Tenso
         want_hist: bool = False, want: tuple[str, ...] = (), chunk_epochs: int = 0,
         workspace: torch.Tensor | None = None, out: dict | None = None,
         phase_ms: list | None = None, capture: list | None = None,
-        single_call: bool = False) -> RunResult:
+        single_call: bool = False, shared_inputs: bool = False) -> RunResult:
     """E epochs of N scenarios. W [E,N,V,M], S [E,N,V] (raw); optional
     B_init [N,V,M] and (Yuma2) normalised Wprev_init [N,V,M].
     single_call: E == 1 through yuma_epoch (one call of a Yuma* variant,
-    yumas.py:61/175/285/399/494) instead of yuma_run."""
+    yumas.py:61/175/285/399/494) instead of yuma_run.
+    shared_inputs: W [E,1,V,M] and S [E,1,V] are one trajectory that every
+    scenario (one per params record) reads — a parameter sweep over one subnet
+    (yuma_run_ex, YUMA_RUN_SHARED_INPUTS); results equal a run on W and S
+    replicated per scenario."""
     dev = device()
     lib = load_library()
-    E, N, V, M = W.shape
-    if S.shape != (E, N, V):
+    E, Nw, V, M = W.shape
+    if S.shape != (E, Nw, V):
         raise ValueError(f"S shape {tuple(S.shape)} does not match W {tuple(W.shape)}")
-    if len(params) != N:
-        raise ValueError("one parameter record per scenario is required")
+    if shared_inputs:
+        if Nw != 1:
+            raise ValueError("shared_inputs takes W [E,1,V,M] and S [E,1,V]")
+        N = len(params)
+        if single_call:
+            raise ValueError("single_call does not take shared inputs")
+    else:
+        N = Nw
+        if len(params) != N:
+            raise ValueError("one parameter record per scenario is required")
     W = _as_dev(W, dev)
     S = _as_dev(S, dev)
     B_init = None if B_init is None else _as_dev(B_init, dev)
@@ -390,8 +409,17 @@ def run(variant: int, params: list[YumaParamsC], W: torch.Tensor, S: torch.Tenso
     elif capture is not None:  # RunGraph: capture instead of launching
         h = ctypes.c_void_p()
         torch.cuda.synchronize(dev)
-        _check(lib.yuma_graph_create(ctypes.byref(h), *args[:-1]), "yuma_graph_create")
+        if shared_inputs:
+            _check(lib.yuma_graph_create_ex(ctypes.byref(h), *args[:-1], RUN_SHARED_INPUTS),
+                   "yuma_graph_create_ex")
+        else:
+            _check(lib.yuma_graph_create(ctypes.byref(h), *args[:-1]), "yuma_graph_create")
         capture.append(h)
+    elif shared_inputs:
+        buf = None if phase_ms is None else (ctypes.c_float * len(PHASES))()
+        _check(lib.yuma_run_ex(*args[:-1], RUN_SHARED_INPUTS, stream, buf), "yuma_run_ex")
+        if phase_ms is not None:
+            phase_ms[:] = list(buf)
     elif phase_ms is None:
         _check(lib.yuma_run(*args), "yuma_run")
     else:  # bench-only: per-phase device time from HIP events (blocks)
