@@ -132,20 +132,6 @@ __device__ __forceinline__ long long in_slice(long long slice, int N, int wsh) {
   return wsh ? slice / N : slice;
 }
 
-// Block -> (slice, sub-block): slice-major; with shared inputs
-// scenario-minor, so the N scenarios' blocks over the same rows / tile of an
-// input slice are consecutive and their reads of it meet in the caches.
-struct SliceBlock {
-  long long slice;
-  int sub;
-};
-__device__ __forceinline__ SliceBlock slice_block(long long slice0, int subs, int N, int wsh) {
-  const long long b = blockIdx.x;
-  if (!wsh) return {slice0 + b / subs, (int)(b % subs)};
-  const long long n = b % N, r = b / N;
-  return {slice0 + (r / subs) * N + n, (int)(r % subs)};
-}
-
 // thread -> (row group g, column quad c4). A wave covers 4 row groups x 64
 // columns, so one float4 load instruction moves 4 x 256 contiguous bytes.
 struct Lay {
@@ -325,10 +311,9 @@ __global__ __launch_bounds__(256) void k_rowsum(const float* __restrict__ W,
                                                 int partial, int* __restrict__ sx, int N,
                                                 int wsh) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const SliceBlock sb = slice_block(slice0, rowblocks, N, wsh);
-  const long long slice = sb.slice;
+  const long long slice = slice0 + blockIdx.x / rowblocks;
   const long long wsl = in_slice(slice, N, wsh);
-  const int rb = sb.sub;
+  const int rb = blockIdx.x % rowblocks;
   const int row = rb * 4 + wave;
   if (row < V) {
     const float* r = W + (wsl * V + row) * (long long)M;
@@ -1009,9 +994,8 @@ __global__ __launch_bounds__(256, 3) void k_consensus_w(const float* __restrict_
                                                      float* __restrict__ Pout, int wsh) {
   __shared__ __attribute__((aligned(16))) unsigned hb[kHistWords];
   const WLay L = wlay();
-  const SliceBlock sb = slice_block(slice0, tiles, N, wsh);
-  const long long slice = sb.slice;
-  const int tile = sb.sub;
+  const long long slice = slice0 + blockIdx.x / tiles;
+  const int tile = blockIdx.x % tiles;
   const int n = (int)(slice % N);
   const int m = tile * kTileM + L.wave * 16 + L.cq * 4;
   if (tile * kTileM + L.wave * 16 >= M) return;  // whole wave past the last miner
@@ -1164,9 +1148,8 @@ __global__ __launch_bounds__(256) void k_rank_s(const float* __restrict__ W,
                                                 float* __restrict__ rpart, int wsh) {
   __shared__ float4 red[4][16];
   const Lay L = lay();
-  const SliceBlock sb = slice_block(slice0, tiles, N, wsh);
-  const long long slice = sb.slice;
-  const int tile = sb.sub;
+  const long long slice = slice0 + blockIdx.x / tiles;
+  const int tile = blockIdx.x % tiles;
   const long long VM = (long long)V * M;
   const int m = tile * kTileM + L.c4 * 4;
   const float* Ws = W + in_slice(slice, N, wsh) * VM;
@@ -1901,12 +1884,9 @@ template <int VARIANT, int R, bool VEC, int P, bool VECI, bool NT = false>
 __global__ __launch_bounds__(256) void k_bonds_elem(BondArgs A) {
   constexpr int G = 16;
   const Lay L = lay();
-  // scenario-minor with shared inputs (slice_block): the scenarios walking one
-  // bond tile read the same W tile at the same epochs
-  const int bx = A.wsh ? (int)(blockIdx.x / A.N) : (int)blockIdx.x;
-  const int tile = bx % A.tiles;
-  const int rb = (bx / A.tiles) % A.rowblocks;
-  const int n = A.wsh ? (int)(blockIdx.x % A.N) : (int)(blockIdx.x / (A.tiles * A.rowblocks));
+  const int tile = blockIdx.x % A.tiles;
+  const int rb = (blockIdx.x / A.tiles) % A.rowblocks;
+  const int n = blockIdx.x / (A.tiles * A.rowblocks);
   const int N = A.N, V = A.V, M = A.M;
   const long long VM = (long long)V * M;
   const int m = tile * kTileM + L.c4 * 4;
