@@ -265,6 +265,14 @@ def sweep_config(g: int):
                                              alpha_low=lo, alpha_high=hi))
 
 
+def consensus_classes(params: list) -> int:
+    """Scenarios of a shared-input run whose consensus the engine computes
+    once (k_classes: equal kappa bits, trip count and histogram switch)."""
+    import struct
+
+    return len({(struct.pack("<f", p.kappa), p.bisect_iters, p.flags & 1) for p in params})
+
+
 def engine_line(args, variant: int, params: list, W, S, world: int, dist: bool, workload: dict,
                 shared: bool = False) -> dict:
     """Time one engine configuration on resident inputs and build its line:
@@ -355,8 +363,13 @@ def engine_line(args, variant: int, params: list, W, S, world: int, dist: bool, 
         },
     }
     if shared:
-        line["roofline"]["note"] = ("every scenario reads one shared W/S trajectory: beyond the epoch-step "
-                                    "contract (SURVEY 8d), so frac counts the contract bytes per scenario-epoch")
+        classes = consensus_classes(params)
+        line["roofline"]["note"] = (
+            "every scenario reads one shared W/S trajectory (beyond the epoch-step contract, SURVEY 8d): the "
+            "row sums run once per input epoch, the consensus search and rank once per consensus class "
+            f"(scenarios with equal kappa and precision: {classes} classes of {N}), bonds per scenario; frac and "
+            "the per-phase GBps count the contract bytes per scenario-epoch, i.e. equivalent rates, not HBM traffic")
+        line["config"]["consensus_classes"] = classes
     line["phases"] = phase_info
     return line
 

@@ -162,19 +162,23 @@ def test_wide_float_weights_against_oracle():
         assert_close(torch.cat(got.B_hist, dim=3)[:, 0].cpu().numpy(), ref["B"], what="B")
 
 
-@pytest.mark.parametrize("variant,extra,reset,chunk", [
-    (engine.VARIANT_YUMA4, {"liquid_alpha": True}, None, 0),
-    (engine.VARIANT_YUMA3, {}, (3, 5), 4),
-    (engine.VARIANT_YUMA2, {"liquid_alpha": True}, None, 3),
-    (engine.VARIANT_RUST, {}, None, 0),
-    (engine.VARIANT_YUMA1, {"bond_penalty": 0.5}, None, 5),
+@pytest.mark.parametrize("variant,extra,reset,chunk,want", [
+    (engine.VARIANT_YUMA4, {"liquid_alpha": True}, None, 0, ("R", "D")),
+    (engine.VARIANT_YUMA3, {}, (3, 5), 4, ("R", "D")),
+    (engine.VARIANT_YUMA3, {}, None, 0, ("R", "D", "T", "Tv")),
+    (engine.VARIANT_YUMA2, {"liquid_alpha": True}, None, 3, ("R", "D")),
+    (engine.VARIANT_RUST, {}, None, 0, ("R", "D")),
+    (engine.VARIANT_YUMA1, {"bond_penalty": 0.5}, None, 5, ("R", "D")),
 ])
-def test_shared_input_sweep_equals_replicated(variant, extra, reset, chunk):
+def test_shared_input_sweep_equals_replicated(variant, extra, reset, chunk, want):
     """yuma_run_ex(YUMA_RUN_SHARED_INPUTS): N scenarios reading ONE W/S
     trajectory ([E,1,V,M]) give bitwise the results of the same run on W and S
     replicated per scenario — consensus, bonds and their history, dividends,
     incentive — with resets, chunking and Yuma2's W_prev; and scenario 0
-    matches the oracle (c3's sweep over one subnet)."""
+    matches the oracle (c3's sweep over one subnet). κ repeats
+    across scenarios (three consensus classes of two, k_classes: the second of
+    each takes the first's consensus, quantisation input and rank); with P / T
+    / T_v requested every scenario computes its own."""
     E, N, V, M = 10, 6, 64, 512
     seed = 0x5EED0003
     W1 = engine.synth_weights(seed, E, 1, V, M)
@@ -183,21 +187,22 @@ def test_shared_input_sweep_equals_replicated(variant, extra, reset, chunk):
     for i in range(N):
         sim = {k: v for k, v in extra.items() if k in ("bond_penalty",)}
         prm = {k: v for k, v in extra.items() if k not in ("bond_penalty",)}
-        cfgs.append(YumaConfig(simulation=bench_sim(kappa=0.3 + 0.08 * i, **sim),
+        cfgs.append(YumaConfig(simulation=bench_sim(kappa=0.3 + 0.08 * (i % 3), **sim),
                                yuma_params=YumaParams(bond_alpha=0.05 + 0.05 * i, **prm)))
     kw = {}
     if reset is not None:
         kw = {"reset_mode": engine.RESET_ALWAYS, "reset_epoch": reset[0], "reset_index": reset[1],
               "n_miners": M, "n_epochs": E}
     params = [engine.make_params(variant, c, **kw) for c in cfgs]
-    a = engine.run(variant, params, W1, S1, want_hist=True, want=("R", "D"), chunk_epochs=chunk,
+    a = engine.run(variant, params, W1, S1, want_hist=True, want=want, chunk_epochs=chunk,
                    shared_inputs=True)
     b = engine.run(variant, params, W1.expand(E, N, V, M).contiguous(), S1.expand(E, N, V).contiguous(),
-                   want_hist=True, want=("R", "D"), chunk_epochs=chunk)
+                   want_hist=True, want=want, chunk_epochs=chunk)
     torch.cuda.synchronize()
-    for x, y in ((a.C, b.C), (a.Dn, b.Dn), (a.I, b.I), (a.B_hist, b.B_hist), (a.B_final, b.B_final),
-                 (a.extra["R"], b.extra["R"]), (a.extra["D"], b.extra["D"])):
+    for x, y in ((a.C, b.C), (a.Dn, b.Dn), (a.I, b.I), (a.B_hist, b.B_hist), (a.B_final, b.B_final)):
         assert torch.equal(x, y)
+    for k in want:
+        assert torch.equal(a.extra[k], b.extra[k]), k
     version = {engine.VARIANT_RUST: "Yuma 0 (subtensor)", engine.VARIANT_YUMA1: "Yuma 1 (paper)",
                engine.VARIANT_YUMA2: "Yuma 2 (Adrian-Fish)", engine.VARIANT_YUMA3: "Yuma 3 (Rhef)",
                engine.VARIANT_YUMA4: "Yuma 4 (Rhef+relative bonds)"}[variant]

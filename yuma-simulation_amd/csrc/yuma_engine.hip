@@ -132,6 +132,42 @@ __device__ __forceinline__ long long in_slice(long long slice, int N, int wsh) {
   return wsh ? slice / N : slice;
 }
 
+// Consensus classes of a shared-input run: with one input trajectory, the
+// consensus, its quantisation and the rank of scenario n depend only on the
+// parameters the search reads (κ, the bisection trip count, the histogram
+// switch), so crep[n] = the first scenario with the same ones; the others
+// take its results (bitwise the same computation). Every other parameter
+// (bond α, liquid α, resets, ...) stays per scenario.
+__global__ __launch_bounds__(256) void k_classes(const yuma_params_t* __restrict__ prm, int N,
+                                                 int* __restrict__ crep) {
+  for (int n = blockIdx.x * 256 + threadIdx.x; n < N; n += gridDim.x * 256) {
+    const yuma_params_t& a = prm[n];
+    const unsigned ka = __float_as_uint(a.kappa), ha = a.flags & YUMA_FLAG_NO_HIST;
+    int r = n;
+    for (int j = 0; j < n; ++j) {
+      const yuma_params_t& b = prm[j];
+      if (__float_as_uint(b.kappa) == ka && b.bisect_iters == a.bisect_iters &&
+          (b.flags & YUMA_FLAG_NO_HIST) == ha) {
+        r = j;
+        break;
+      }
+    }
+    crep[n] = r;
+  }
+}
+// is slice (t, n) computed by another scenario's block (crep[n] != n)?
+__device__ __forceinline__ bool dup_slice(const int* crep, long long slice, int N) {
+  if (crep == nullptr) return false;
+  const int n = (int)(slice % N);
+  return crep[n] != n;
+}
+// the slice whose consensus / rank results slice (t, n) takes
+__device__ __forceinline__ long long rep_slice(const int* crep, long long slice, int N) {
+  if (crep == nullptr) return slice;
+  const int n = (int)(slice % N);
+  return slice - n + crep[n];
+}
+
 // thread -> (row group g, column quad c4). A wave covers 4 row groups x 64
 // columns, so one float4 load instruction moves 4 x 256 contiguous bytes.
 struct Lay {
@@ -306,13 +342,15 @@ __device__ __forceinline__ void load4_vec(const float* __restrict__ v, int m, in
 template <bool VEC>
 __global__ __launch_bounds__(256) void k_rowsum(const float* __restrict__ W,
                                                 const float* __restrict__ S, int V, int M,
-                                                long long slice0, int rowblocks,
+                                                long long islice0, int rowblocks,
                                                 float* __restrict__ rsd, float* __restrict__ sn,
-                                                int partial, int* __restrict__ sx, int N,
-                                                int wsh) {
+                                                int partial, int* __restrict__ sx, int fan) {
+  // Block = 4 rows of input slice wsl. Its row sums and normalised stakes
+  // belong to output slices wsl·fan .. wsl·fan + fan - 1: fan = 1, or N with
+  // shared inputs (they do not depend on the scenario: computed once, stored
+  // for every scenario).
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const long long slice = slice0 + blockIdx.x / rowblocks;
-  const long long wsl = in_slice(slice, N, wsh);
+  const long long wsl = islice0 + blockIdx.x / rowblocks;
   const int rb = blockIdx.x % rowblocks;
   const int row = rb * 4 + wave;
   if (row < V) {
@@ -340,9 +378,12 @@ __global__ __launch_bounds__(256) void k_rowsum(const float* __restrict__ W,
       acc = acc + q;
     }
     // partial (column shard): the caller sums the shards, then k_add_eps
-    if (lane == 0) rsd[slice * V + row] = partial ? acc : acc + 1e-6f;
+    const float rs = partial ? acc : acc + 1e-6f;
+    for (int f = lane; f < fan; f += 64) rsd[(wsl * fan + f) * V + row] = rs;
   }
-  if (rb == 0 && wave == 0) {
+  // the stake normalisation: output slices f = rb, rb + rowblocks, ... of
+  // the fan (block 0 alone when fan = 1)
+  if (rb < fan && wave == 0) {
     const float* s = S + wsl * V;
     float acc = 0.0f;
     for (int v = lane; v < V; v += 64) acc = acc + s[v];
@@ -354,14 +395,15 @@ __global__ __launch_bounds__(256) void k_rowsum(const float* __restrict__ W,
     bool exact = true;
     for (int v = lane; v < V; v += 64) {
       const float q = s[v] / acc;
-      sn[slice * V + v] = q;
+      for (int f = rb; f < fan; f += rowblocks) sn[(wsl * fan + f) * V + v] = q;
       const float f = q * 16777216.0f;
       exact &= f >= 0.0f && f <= 16777216.0f && __builtin_amdgcn_fractf(f) == 0.0f;
       units += exact ? (int)f : 0;
     }
     for (int o = 1; o < 64; o <<= 1) units += __shfl_xor(units, o, 64);
     exact = __all(exact) && units <= (1 << 24);
-    if (lane == 0) sx[slice] = exact ? units : -1;
+    if (lane == 0)
+      for (int f = rb; f < fan; f += rowblocks) sx[wsl * fan + f] = exact ? units : -1;
   }
 }
 
@@ -379,13 +421,15 @@ __global__ __launch_bounds__(NT) void k_consensus(const float* __restrict__ W,
                                                   const yuma_params_t* __restrict__ prm, int N,
                                                   int V, int M, long long slice0, int tiles,
                                                   double* __restrict__ craw,
-                                                  float* __restrict__ Pout, int wsh) {
+                                                  float* __restrict__ Pout, int wsh,
+                                                  const int* __restrict__ crep) {
   constexpr int NW = NT / 64, G = NT / 16;
   __shared__ float4 red[2][NW * 16];
   const Lay L = lay();
   const long long slice = slice0 + blockIdx.x / tiles;
   const int tile = blockIdx.x % tiles;
   const int n = (int)(slice % N);
+  if (dup_slice(crep, slice, N)) return;  // block-uniform
   const int m = tile * kTileM + L.c4 * 4;
   const float* Ws = W + in_slice(slice, N, wsh) * (long long)V * M;
 
@@ -991,12 +1035,14 @@ __global__ __launch_bounds__(256, 3) void k_consensus_w(const float* __restrict_
                                                      const yuma_params_t* __restrict__ prm, int N,
                                                      int V, int M, long long slice0, int tiles,
                                                      double* __restrict__ craw,
-                                                     float* __restrict__ Pout, int wsh) {
+                                                     float* __restrict__ Pout, int wsh,
+                                                     const int* __restrict__ crep) {
   __shared__ __attribute__((aligned(16))) unsigned hb[kHistWords];
   const WLay L = wlay();
   const long long slice = slice0 + blockIdx.x / tiles;
   const int tile = blockIdx.x % tiles;
   const int n = (int)(slice % N);
+  if (dup_slice(crep, slice, N)) return;  // block-uniform
   const int m = tile * kTileM + L.wave * 16 + L.cq * 4;
   if (tile * kTileM + L.wave * 16 >= M) return;  // whole wave past the last miner
   float wn[R][4], s[R];
@@ -1145,11 +1191,13 @@ __global__ __launch_bounds__(256) void k_rank_s(const float* __restrict__ W,
                                                 const float* __restrict__ C, int N, int V, int M,
                                                 long long slice0, int tiles,
                                                 float* __restrict__ Rout,
-                                                float* __restrict__ rpart, int wsh) {
+                                                float* __restrict__ rpart, int wsh,
+                                                const int* __restrict__ crep) {
   __shared__ float4 red[4][16];
   const Lay L = lay();
   const long long slice = slice0 + blockIdx.x / tiles;
   const int tile = blockIdx.x % tiles;
+  if (dup_slice(crep, slice, N)) return;  // block-uniform
   const long long VM = (long long)V * M;
   const int m = tile * kTileM + L.c4 * 4;
   const float* Ws = W + in_slice(slice, N, wsh) * VM;
@@ -1308,13 +1356,13 @@ __global__ __launch_bounds__(NT) void k_quantise(const double* __restrict__ craw
                                                  float* __restrict__ scal,
                                                  const float* __restrict__ ext_sumf,
                                                  const double* __restrict__ ext_sumd,
-                                                 int no_liquid) {
+                                                 int no_liquid, const int* __restrict__ crep) {
   __shared__ float redf[NT / 64];
   __shared__ double redd[NT / 64];
   __shared__ int hist1[256], hist2[256], bc[4];
   const long long slice = slice0 + blockIdx.x;
   const yuma_params_t& p = prm[slice % N];
-  const double* cr = craw + slice * M;
+  const double* cr = craw + rep_slice(crep, slice, N) * M;
   int* q = qlev + slice * M;
   float* Cs = C + slice * M;
 
@@ -1554,28 +1602,32 @@ __global__ __launch_bounds__(NT) void k_liquid(const yuma_params_t* __restrict__
 // Phase 1e, one block per slice: I = nan_to_num(R / R.sum(), 0) and the
 // server trust T = nan_to_num(R / P) (yumas.py:220-223).
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_incentive(const float* __restrict__ Rin,
+__global__ __launch_bounds__(256) void k_incentive(float* __restrict__ Rio,
                                                    const float* __restrict__ rpart,
                                                    const float* __restrict__ Pin, int M,
                                                    long long slice0, int tiles,
                                                    float* __restrict__ I, float* __restrict__ T,
                                                    float* __restrict__ scal,
-                                                   const float* __restrict__ ext_rsum) {
+                                                   const float* __restrict__ ext_rsum,
+                                                   const int* __restrict__ crep, int N) {
   __shared__ float tot;
   const long long slice = slice0 + blockIdx.x;
+  // rank computed by the class representative (crep): R copied into this slice
+  const long long rs = rep_slice(crep, slice, N);
   if (threadIdx.x == 0) {
     float s = 0.0f;
     if (ext_rsum != nullptr)  // miner-column shard: sum over every shard
       s = ext_rsum[slice];
     else
-      for (int k = 0; k < tiles; ++k) s = s + rpart[slice * tiles + k];
+      for (int k = 0; k < tiles; ++k) s = s + rpart[rs * tiles + k];
     tot = s;
     scal[slice * 8 + 5] = s;
   }
   __syncthreads();
   const float sr = tot;
   for (int m = threadIdx.x; m < M; m += 256) {
-    const float r = Rin[slice * M + m];
+    const float r = Rio[rs * M + m];
+    if (rs != slice) Rio[slice * M + m] = r;
     I[slice * M + m] = nan_to_num(r / sr, 0.0f);
     if (T != nullptr) T[slice * M + m] = nan_to_num(r / Pin[slice * M + m], 0.0f);
   }
@@ -2216,6 +2268,7 @@ struct Workspace {
   float* Bstate;
   float* sumc_f;
   double* sumc_d;
+  int* crep;  // per scenario: consensus class representative (k_classes)
   size_t bytes;
 };
 
@@ -2247,6 +2300,7 @@ Workspace carve(char* base, int variant, int N, int E, int V, int M, int full) {
   w.Bstate = (float*)take((size_t)N * V * M * 4);
   w.sumc_f = (float*)take(S * 4);
   w.sumc_d = (double*)take(S * 8);
+  w.crep = (int*)take((size_t)N * 4);
   w.bytes = off;
   return w;
 }
@@ -2268,28 +2322,29 @@ RowCfg row_cfg(int V) {
 template <int R, bool VEC>
 void launch_consensus_w(long long nblocks, hipStream_t st, const float* W, const float* rsd,
                         const float* sn, const int* sx, const yuma_params_t* prm, int N, int V,
-                        int M, long long slice0, int tiles, double* craw, float* P, int wsh) {
+                        int M, long long slice0, int tiles, double* craw, float* P, int wsh,
+                        const int* crep) {
   YK_LAUNCH((yk::k_consensus_w<R, VEC>), nblocks, 256, st, W, rsd, sn, sx, prm, N, V, M, slice0,
-            tiles, craw, P, wsh);
+            tiles, craw, P, wsh, crep);
 }
 
 template <bool VEC>
 void launch_consensus(RowCfg rc, long long nblocks, hipStream_t st, const float* W,
                       const float* rsd, const float* sn, const int* sx,
                       const yuma_params_t* prm, int N, int V, int M, long long slice0, int tiles,
-                      double* craw, float* P, int wsh) {
+                      double* craw, float* P, int wsh, const int* crep) {
   switch (rc) {  // wave-owned columns up to 256 validators
     case RC_256_1:
       launch_consensus_w<1, VEC>(nblocks, st, W, rsd, sn, sx, prm, N, V, M, slice0, tiles, craw,
-                                  P, wsh);
+                                  P, wsh, crep);
       return;
     case RC_256_4:
       launch_consensus_w<4, VEC>(nblocks, st, W, rsd, sn, sx, prm, N, V, M, slice0, tiles, craw,
-                                  P, wsh);
+                                  P, wsh, crep);
       return;
     case RC_256_16:
       launch_consensus_w<16, VEC>(nblocks, st, W, rsd, sn, sx, prm, N, V, M, slice0, tiles, craw,
-                                  P, wsh);
+                                  P, wsh, crep);
       return;
     default:
       break;
@@ -2297,19 +2352,19 @@ void launch_consensus(RowCfg rc, long long nblocks, hipStream_t st, const float*
   switch (rc) {
     case RC_256_1:
       YK_LAUNCH((yk::k_consensus<256, 1, VEC>), nblocks, 256, st, W, rsd, sn, prm, N, V, M,
-                slice0, tiles, craw, P, wsh);
+                slice0, tiles, craw, P, wsh, crep);
       break;
     case RC_256_4:
       YK_LAUNCH((yk::k_consensus<256, 4, VEC>), nblocks, 256, st, W, rsd, sn, prm, N, V, M,
-                slice0, tiles, craw, P, wsh);
+                slice0, tiles, craw, P, wsh, crep);
       break;
     case RC_256_16:
       YK_LAUNCH((yk::k_consensus<256, 16, VEC>), nblocks, 256, st, W, rsd, sn, prm, N, V, M,
-                slice0, tiles, craw, P, wsh);
+                slice0, tiles, craw, P, wsh, crep);
       break;
     case RC_1024_16:
       YK_LAUNCH((yk::k_consensus<1024, 16, VEC>), nblocks, 1024, st, W, rsd, sn, prm, N, V, M,
-                slice0, tiles, craw, P, wsh);
+                slice0, tiles, craw, P, wsh, crep);
       break;
   }
 }
@@ -2318,10 +2373,11 @@ template <bool VEC>
 void launch_rank(RowCfg rc, long long nblocks, hipStream_t st, const float* W, const float* rsd,
                  const float* sn, const float* C, const float* Wprev_init, int yuma2, int N,
                  int V, int M, long long slice0, int tiles, float* R, float* rpart, float* Wn,
-                 float* Wc, float* tvc, float* tvn, int wsh) {
+                 float* Wc, float* tvc, float* tvn, int wsh, const int* crep = nullptr) {
   const bool full = Wn != nullptr || Wc != nullptr || tvc != nullptr;
   if (!full && !yuma2) {  // streaming rank; k_rank_w also materialises Wn / Wc / T_v or clips W_prev
-    YK_LAUNCH(yk::k_rank_s<VEC>, nblocks, 256, st, W, rsd, sn, C, N, V, M, slice0, tiles, R, rpart, wsh);
+    YK_LAUNCH(yk::k_rank_s<VEC>, nblocks, 256, st, W, rsd, sn, C, N, V, M, slice0, tiles, R, rpart,
+              wsh, crep);
     return;
   }
   auto go = [&](auto kern) {
@@ -2490,6 +2546,20 @@ int run_impl(int variant, const yuma_params_t* prm, int N, int E, int V, int M, 
   const int brows = 16 * bonds_rows(vec, out->B_hist != nullptr);  // rows per bond block
   const int rowblocks = colnorm ? 1 : (V + brows - 1) / brows;
 
+  // Shared inputs: scenarios with the same consensus parameters take one
+  // representative's consensus, quantisation input and (streaming) rank
+  // (k_classes). Off when the prerank P is requested (the consensus pass
+  // writes it for every slice) and for the materialising / Yuma2 rank.
+  const int* crep = nullptr;
+  if (wsh && N > 1 && out->P == nullptr) {
+    const long long nb = (N + 255) / 256;
+    YK_LAUNCH(yk::k_classes, nb < 64 ? nb : 64, 256, st, prm, N, ws.crep);
+    crep = ws.crep;
+  }
+  const bool rank_stream = out->Wn == nullptr && out->Wc == nullptr && ws.tvc == nullptr &&
+                           variant != YUMA_VARIANT_YUMA2;
+  const int* rcrep = rank_stream ? crep : nullptr;
+
   PhaseTimer tm{};
   tm.ms = phase_ms;
   tm.st = st;
@@ -2500,36 +2570,39 @@ int run_impl(int variant, const yuma_params_t* prm, int N, int E, int V, int M, 
     const long long ns = (long long)(c1 - c0) * N;
     {
       const int rowblocks4 = (V + 3) / 4;
+      // shared inputs: one row-sum pass per input epoch, stored for all N
+      const long long rs_in = wsh ? c1 - c0 : ns, rs_s0 = wsh ? c0 : s0;
+      const int fan = wsh ? N : 1;
       tm.mark(YUMA_PHASE_ROWSUM);
       if (vec)
-        YK_LAUNCH(yk::k_rowsum<true>, ns * rowblocks4, 256, st, W, S, V, M, s0, rowblocks4,
-                  ws.rsd, ws.sn, 0, ws.sx, N, wsh);
+        YK_LAUNCH(yk::k_rowsum<true>, rs_in * rowblocks4, 256, st, W, S, V, M, rs_s0, rowblocks4,
+                  ws.rsd, ws.sn, 0, ws.sx, fan);
       else
-        YK_LAUNCH(yk::k_rowsum<false>, ns * rowblocks4, 256, st, W, S, V, M, s0, rowblocks4,
-                  ws.rsd, ws.sn, 0, ws.sx, N, wsh);
+        YK_LAUNCH(yk::k_rowsum<false>, rs_in * rowblocks4, 256, st, W, S, V, M, rs_s0,
+                  rowblocks4, ws.rsd, ws.sn, 0, ws.sx, fan);
       tm.mark(YUMA_PHASE_CONSENSUS);
       if (vec)
         launch_consensus<true>(rc, ns * tiles, st, W, ws.rsd, ws.sn, ws.sx, prm, N, V, M, s0, tiles,
-                               ws.craw, out->P, wsh);
+                               ws.craw, out->P, wsh, crep);
       else
         launch_consensus<false>(rc, ns * tiles, st, W, ws.rsd, ws.sn, ws.sx, prm, N, V, M, s0,
-                                tiles, ws.craw, out->P, wsh);
+                                tiles, ws.craw, out->P, wsh, crep);
       tm.mark(YUMA_PHASE_QUANTISE);
       YK_LAUNCH(yk::k_quantise<256>, ns, 256, st, ws.craw, prm, variant, N, M, s0, C, ws.qlev,
-                ba_buf, ws.scal, nullptr, nullptr, 0);
+                ba_buf, ws.scal, nullptr, nullptr, 0, crep);
       tm.mark(YUMA_PHASE_RANK);
       if (vec)
         launch_rank<true>(rc, ns * tiles, st, W, ws.rsd, ws.sn, C, Wprev_init,
                           variant == YUMA_VARIANT_YUMA2, N, V, M, s0, tiles, Rr, ws.rpart, out->Wn,
-                          out->Wc, ws.tvc, ws.tvn, wsh);
+                          out->Wc, ws.tvc, ws.tvn, wsh, rcrep);
       else
         launch_rank<false>(rc, ns * tiles, st, W, ws.rsd, ws.sn, C, Wprev_init,
                            variant == YUMA_VARIANT_YUMA2, N, V, M, s0, tiles, Rr, ws.rpart,
-                           out->Wn, out->Wc, ws.tvc, ws.tvn, wsh);
+                           out->Wn, out->Wc, ws.tvc, ws.tvn, wsh, rcrep);
     }
     tm.mark(YUMA_PHASE_INCENTIVE);
     YK_LAUNCH(yk::k_incentive, ns, 256, st, Rr, ws.rpart, out->P, M, s0, tiles, I,
-              out->P ? out->T : nullptr, ws.scal, nullptr);
+              out->P ? out->T : nullptr, ws.scal, nullptr, rcrep, N);
 
     yk::BondArgs A{};
     A.W = W;
@@ -2635,10 +2708,10 @@ int shard_stage_impl(int stage, int variant, const yuma_params_t* prm, int N, in
       const int rb4 = (V + 3) / 4;
       if (vec)
         YK_LAUNCH(yk::k_rowsum<true>, ns * rb4, 256, st, W, S, V, M, 0LL, rb4, io->rowsum_part,
-                  ws.sn, 1, ws.sx, N, 0);
+                  ws.sn, 1, ws.sx, 1);
       else
         YK_LAUNCH(yk::k_rowsum<false>, ns * rb4, 256, st, W, S, V, M, 0LL, rb4, io->rowsum_part,
-                  ws.sn, 1, ws.sx, N, 0);
+                  ws.sn, 1, ws.sx, 1);
       break;
     }
     case 2: {
@@ -2649,10 +2722,10 @@ int shard_stage_impl(int stage, int variant, const yuma_params_t* prm, int N, in
       YK_LAUNCH(yk::k_add_eps, nb, 256, st, io->rowsum, ns * V, ws.rsd);
       if (vec)
         launch_consensus<true>(rc, ns * tiles, st, W, ws.rsd, ws.sn, ws.sx, prm, N, V, M, 0LL, tiles,
-                               ws.craw, out->P, 0);
+                               ws.craw, out->P, 0, nullptr);
       else
         launch_consensus<false>(rc, ns * tiles, st, W, ws.rsd, ws.sn, ws.sx, prm, N, V, M, 0LL, tiles,
-                                ws.craw, out->P, 0);
+                                ws.craw, out->P, 0, nullptr);
       YK_LAUNCH(yk::k_csum, ns, 256, st, ws.craw, rust ? 1 : 0, M, io->csum_part, io->csum_part_d);
       break;
     }
@@ -2660,7 +2733,7 @@ int shard_stage_impl(int stage, int variant, const yuma_params_t* prm, int N, in
       if ((rust ? !io->csum_d : !io->csum) || !io->rsum_part)
         return fail(YUMA_EINVAL, "stage 3 needs io->csum%s and io->rsum_part", rust ? "_d" : "");
       YK_LAUNCH(yk::k_quantise<256>, ns, 256, st, ws.craw, prm, variant, N, M, 0LL, C, qlev,
-                ba_buf, ws.scal, rust ? nullptr : io->csum, rust ? io->csum_d : nullptr, 1);
+                ba_buf, ws.scal, rust ? nullptr : io->csum, rust ? io->csum_d : nullptr, 1, nullptr);
       if (vec)
         launch_rank<true>(rc, ns * tiles, st, W, ws.rsd, ws.sn, C, Wprev_init,
                           variant == YUMA_VARIANT_YUMA2, N, V, M, 0LL, tiles, R, ws.rpart,
@@ -2681,7 +2754,7 @@ int shard_stage_impl(int stage, int variant, const yuma_params_t* prm, int N, in
                 ba_buf, ws.scal, rust ? nullptr : io->csum, rust ? io->csum_d : nullptr,
                 rust ? 1 : 0);
       YK_LAUNCH(yk::k_incentive, ns, 256, st, R, ws.rpart, out->P, M, 0LL, tiles, I,
-                out->P ? out->T : nullptr, ws.scal, io->rsum);
+                out->P ? out->T : nullptr, ws.scal, io->rsum, nullptr, N);
       yk::BondArgs A{};
       A.W = W;
       A.rsd = ws.rsd;
