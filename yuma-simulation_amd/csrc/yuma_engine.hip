@@ -2072,9 +2072,18 @@ __global__ __launch_bounds__(256) void k_bonds_elem(BondArgs A) {
           }
         }
         float d = 0.0f;
+        // M % 4 == 0: a column quad is wholly in or out. (Not with the
+        // history stream: there the lane branch cost the c2 scan 1.65 ->
+        // 2.71 ms, same box.)
+        if (VEC && !NT) {
+          if (m < M)
 #pragma unroll
-        for (int c = 0; c < 4; ++c)
-          if (m + c < M) d = d + B[i][c] * ri[k][c];
+            for (int c = 0; c < 4; ++c) d = d + B[i][c] * ri[k][c];
+        } else {
+#pragma unroll
+          for (int c = 0; c < 4; ++c)
+            if (m + c < M) d = d + B[i][c] * ri[k][c];
+        }
         d = wsum16(d);  // sum_row16's xor-butterfly tree, on DPP
         if (L.c4 == 0 && row < V) A.dpart[(slice * A.tiles + tile) * V + row] = d;
       }
@@ -2462,13 +2471,19 @@ void launch_bonds_colnorm(RowCfg rc, long long nblocks, hipStream_t st, const yk
 // non-temporal history stores (Yuma3 1.68 ms, Yuma4 liquid 1.72 ms, against
 // 1.81 / 2.66 for R = 1, P = 4 and per-column loads); without the history,
 // R = 1, P = 4 (1.13 ms vs 1.36 for R = 2).
-int bonds_rows(bool vec, bool hist) { return vec && hist ? 2 : 1; }
+// Rows per thread of k_bonds_elem: 2 where the scan has the VALU to spare
+// per column load (the history stream; shared-input sweeps, whose W reads hit
+// the caches, 11.4 -> 10.4 ms at c3), 1 for a bare HBM-bound scan (c2
+// without history: 1.13 vs 1.36 ms).
+int bonds_rows(bool vec, bool hist, bool wsh) { return vec && (hist || wsh) ? 2 : 1; }
 template <int VARIANT, bool VEC>
 void launch_bonds_elem(long long nblocks, hipStream_t st, const yk::BondArgs& A) {
-  if (bonds_rows(VEC, A.B_hist != nullptr) == 2)
+  if (bonds_rows(VEC, A.B_hist != nullptr, A.wsh) != 2)
+    YK_LAUNCH((yk::k_bonds_elem<VARIANT, 1, VEC, 4, VEC, false>), nblocks, 256, st, A);
+  else if (A.B_hist != nullptr)
     YK_LAUNCH((yk::k_bonds_elem<VARIANT, 2, VEC, 2, VEC, true>), nblocks, 256, st, A);
   else
-    YK_LAUNCH((yk::k_bonds_elem<VARIANT, 1, VEC, 4, VEC, false>), nblocks, 256, st, A);
+    YK_LAUNCH((yk::k_bonds_elem<VARIANT, 2, VEC, 2, VEC, false>), nblocks, 256, st, A);
 }
 
 template <bool VEC>
@@ -2557,7 +2572,7 @@ int run_impl(int variant, const yuma_params_t* prm, int N, int E, int V, int M, 
   if (chunk <= 0 || chunk > E) chunk = E;
 
   const int colnorm = variant <= YUMA_VARIANT_YUMA2;
-  const int brows = 16 * bonds_rows(vec, out->B_hist != nullptr);  // rows per bond block
+  const int brows = 16 * bonds_rows(vec, out->B_hist != nullptr, wsh != 0);  // rows per bond block
   const int rowblocks = colnorm ? 1 : (V + brows - 1) / brows;
 
   // Shared inputs: scenarios with the same consensus parameters take one
@@ -2788,7 +2803,7 @@ int shard_stage_impl(int stage, int variant, const yuma_params_t* prm, int N, in
       A.V = V;
       A.M = M;
       A.tiles = tiles;
-      const int brows = 16 * bonds_rows(vec, out->B_hist != nullptr);
+      const int brows = 16 * bonds_rows(vec, out->B_hist != nullptr, false);
       A.rowblocks = variant <= YUMA_VARIANT_YUMA2 ? 1 : (V + brows - 1) / brows;
       A.t0 = 0;
       A.t1 = E;
