@@ -356,6 +356,7 @@ __global__ __launch_bounds__(256) void k_rowsum(const float* __restrict__ W,
   if (row < V) {
     const float* r = W + (wsl * V + row) * (long long)M;
     float acc = 0.0f;
+#pragma unroll 4
     for (int m0 = 0; m0 < M; m0 += 256) {
       const int m = m0 + lane * 4;
       float x[4];
@@ -1602,6 +1603,7 @@ __global__ __launch_bounds__(NT) void k_liquid(const yuma_params_t* __restrict__
 // Phase 1e, one block per slice: I = nan_to_num(R / R.sum(), 0) and the
 // server trust T = nan_to_num(R / P) (yumas.py:220-223).
 // ---------------------------------------------------------------------------
+constexpr int kIncCols = 4096;
 __global__ __launch_bounds__(256) void k_incentive(float* __restrict__ Rio,
                                                    const float* __restrict__ rpart,
                                                    const float* __restrict__ Pin, int M,
@@ -1609,23 +1611,40 @@ __global__ __launch_bounds__(256) void k_incentive(float* __restrict__ Rio,
                                                    float* __restrict__ I, float* __restrict__ T,
                                                    float* __restrict__ scal,
                                                    const float* __restrict__ ext_rsum,
-                                                   const int* __restrict__ crep, int N) {
+                                                   const int* __restrict__ crep, int N,
+                                                   int nchunk) {
+  // block = (slice, chunk of kIncCols miners): every block of a slice forms
+  // the same ΣR (same order, same bits), then scales its own chunk
+  constexpr int kStage = 4096;
   __shared__ float tot;
-  const long long slice = slice0 + blockIdx.x;
+  __shared__ float rp[kStage];
+  const long long slice = slice0 + blockIdx.x / nchunk;
+  const int ch = blockIdx.x % nchunk;
   // rank computed by the class representative (crep): R copied into this slice
   const long long rs = rep_slice(crep, slice, N);
+  float s = 0.0f;
+  if (ext_rsum != nullptr) {  // miner-column shard: sum over every shard
+    s = ext_rsum[slice];
+  } else {
+    // the tile partials staged through LDS by the whole block (a wide subnet
+    // has 1024 per slice), summed in tile order by one thread
+    for (int k0 = 0; k0 < tiles; k0 += kStage) {
+      const int nk = tiles - k0 < kStage ? tiles - k0 : kStage;
+      for (int k = threadIdx.x; k < nk; k += 256) rp[k] = rpart[rs * tiles + k0 + k];
+      __syncthreads();
+      if (threadIdx.x == 0)
+        for (int k = 0; k < nk; ++k) s = s + rp[k];
+      __syncthreads();
+    }
+  }
   if (threadIdx.x == 0) {
-    float s = 0.0f;
-    if (ext_rsum != nullptr)  // miner-column shard: sum over every shard
-      s = ext_rsum[slice];
-    else
-      for (int k = 0; k < tiles; ++k) s = s + rpart[rs * tiles + k];
     tot = s;
-    scal[slice * 8 + 5] = s;
+    if (ch == 0) scal[slice * 8 + 5] = s;
   }
   __syncthreads();
   const float sr = tot;
-  for (int m = threadIdx.x; m < M; m += 256) {
+  const int m1 = min(M, (ch + 1) * kIncCols);
+  for (int m = ch * kIncCols + threadIdx.x; m < m1; m += 256) {
     const float r = Rio[rs * M + m];
     if (rs != slice) Rio[slice * M + m] = r;
     I[slice * M + m] = nan_to_num(r / sr, 0.0f);
@@ -2121,11 +2140,25 @@ __global__ __launch_bounds__(256) void k_finalize(const float* __restrict__ dpar
   const float* dp = dpart + slice * (long long)tiles * V;
   for (int v0 = 0; v0 < V; v0 += 256) {
     float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-    for (int k = tg; k < tiles; k += 4) {
+    const int vb = v0 + vq * 4;
+    if ((V & 3) == 0 && vb < V) {
+      // whole validator quads: float4 loads, 8 tiles in flight (a wide
+      // subnet has 1024 tiles per slice; same per-group sequential order)
+#pragma unroll 8
+      for (int k = tg; k < tiles; k += 4) {
+        const float4 x = *reinterpret_cast<const float4*>(dp + (long long)k * V + vb);
+        acc[0] = acc[0] + x.x;
+        acc[1] = acc[1] + x.y;
+        acc[2] = acc[2] + x.z;
+        acc[3] = acc[3] + x.w;
+      }
+    } else {
+      for (int k = tg; k < tiles; k += 4) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int v = v0 + vq * 4 + j;
-        if (v < V) acc[j] = acc[j] + dp[(long long)k * V + v];
+        for (int j = 0; j < 4; ++j) {
+          const int v = vb + j;
+          if (v < V) acc[j] = acc[j] + dp[(long long)k * V + v];
+        }
       }
     }
 #pragma unroll
@@ -2630,8 +2663,9 @@ int run_impl(int variant, const yuma_params_t* prm, int N, int E, int V, int M, 
                            out->Wn, out->Wc, ws.tvc, ws.tvn, wsh, rcrep);
     }
     tm.mark(YUMA_PHASE_INCENTIVE);
-    YK_LAUNCH(yk::k_incentive, ns, 256, st, Rr, ws.rpart, out->P, M, s0, tiles, I,
-              out->P ? out->T : nullptr, ws.scal, nullptr, rcrep, N);
+    const int ich = (M + yk::kIncCols - 1) / yk::kIncCols;
+    YK_LAUNCH(yk::k_incentive, ns * ich, 256, st, Rr, ws.rpart, out->P, M, s0, tiles, I,
+              out->P ? out->T : nullptr, ws.scal, nullptr, rcrep, N, ich);
 
     yk::BondArgs A{};
     A.W = W;
@@ -2782,8 +2816,9 @@ int shard_stage_impl(int stage, int variant, const yuma_params_t* prm, int N, in
       YK_LAUNCH(yk::k_liquid<256>, ns, 256, st, prm, N, M, 0LL, C, io->levels_all, io->M_total,
                 ba_buf, ws.scal, rust ? nullptr : io->csum, rust ? io->csum_d : nullptr,
                 rust ? 1 : 0);
-      YK_LAUNCH(yk::k_incentive, ns, 256, st, R, ws.rpart, out->P, M, 0LL, tiles, I,
-                out->P ? out->T : nullptr, ws.scal, io->rsum, nullptr, N);
+      const int ich = (M + yk::kIncCols - 1) / yk::kIncCols;
+      YK_LAUNCH(yk::k_incentive, ns * ich, 256, st, R, ws.rpart, out->P, M, 0LL, tiles, I,
+                out->P ? out->T : nullptr, ws.scal, io->rsum, nullptr, N, ich);
       yk::BondArgs A{};
       A.W = W;
       A.rsd = ws.rsd;
