@@ -228,3 +228,18 @@ def test_bench_line_helpers():
     assert pmc is not None and pmc["k_bonds_elem"] > 8e6
     assert bench.load_traffic(dict(key, M=1)) is None
     assert bench.contract_bytes(256, 4096, 3) == 12_617_728
+
+
+def test_bench_consensus_classes():
+    """The c3 line's consensus-class count (what k_classes shares on the GPU:
+    equal kappa bits, bisection trip count and histogram switch): 16 kappa
+    values per GPU share of the 4096-point grid."""
+    import sys
+
+    sys.path.insert(0, ROOT)
+    import bench
+
+    params = [engine.make_params(engine.VARIANT_YUMA4, bench.sweep_config(g)) for g in range(512)]
+    assert bench.consensus_classes(params) == 16
+    params[3].flags |= engine.FLAG_NO_HIST  # the histogram switch splits a class
+    assert bench.consensus_classes(params) == 17
