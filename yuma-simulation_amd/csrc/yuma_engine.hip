@@ -339,21 +339,61 @@ __device__ __forceinline__ void load4_vec(const float* __restrict__ v, int m, in
 // ((x0+x1)+x2)+x3 (lane l holds quad l: the 64-lane butterfly); the chunk
 // partials are added in chunk order.
 // ---------------------------------------------------------------------------
-template <bool VEC>
+// WIDE (rows of >= kWideChunks chunks, e.g. a 65536-miner subnet): block =
+// ONE row, its chunks dealt to the 4 waves, the chunk partials parked in LDS
+// and added in chunk order by one lane — the same bits, and 4x the blocks
+// (one long wave per row leaves the last of ~3 dispatch rounds mostly idle).
+constexpr int kWideChunks = 64, kMaxWideChunks = 4096;
+template <bool VEC, bool WIDE = false>
 __global__ __launch_bounds__(256) void k_rowsum(const float* __restrict__ W,
                                                 const float* __restrict__ S, int V, int M,
                                                 long long islice0, int rowblocks,
                                                 float* __restrict__ rsd, float* __restrict__ sn,
                                                 int partial, int* __restrict__ sx, int fan) {
-  // Block = 4 rows of input slice wsl. Its row sums and normalised stakes
-  // belong to output slices wsl·fan .. wsl·fan + fan - 1: fan = 1, or N with
-  // shared inputs (they do not depend on the scenario: computed once, stored
-  // for every scenario).
+  // Block = 4 rows (WIDE: one row) of input slice wsl. Its row sums and
+  // normalised stakes belong to output slices wsl·fan .. wsl·fan + fan - 1:
+  // fan = 1, or N with shared inputs (they do not depend on the scenario:
+  // computed once, stored for every scenario).
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const long long wsl = islice0 + blockIdx.x / rowblocks;
   const int rb = blockIdx.x % rowblocks;
+  if constexpr (WIDE) {
+    __shared__ float qs[kMaxWideChunks];
+    const int nc = (M + 255) / 256;
+    const float* r = W + (wsl * V + rb) * (long long)M;
+#pragma unroll 4
+    for (int k = wave; k < nc; k += 4) {
+      const int m = k * 256 + lane * 4;
+      float x[4];
+      if (VEC) {
+        if (m < M) {
+          const float4 t = *reinterpret_cast<const float4*>(r + m);
+          x[0] = t.x;
+          x[1] = t.y;
+          x[2] = t.z;
+          x[3] = t.w;
+        } else {
+          x[0] = x[1] = x[2] = x[3] = 0.0f;
+        }
+      } else {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) x[c] = m + c < M ? r[m + c] : 0.0f;
+      }
+      const float q = wave_sum(((x[0] + x[1]) + x[2]) + x[3]);
+      if (lane == 0) qs[k] = q;
+    }
+    __syncthreads();
+    if (wave == 0) {
+      float acc = 0.0f;
+      if (lane == 0)
+        for (int k = 0; k < nc; ++k) acc = acc + qs[k];
+      acc = __shfl(acc, 0, 64);
+      const float rs = partial ? acc : acc + 1e-6f;
+      for (int f = lane; f < fan; f += 64) rsd[(wsl * fan + f) * V + rb] = rs;
+    }
+  }
   const int row = rb * 4 + wave;
-  if (row < V) {
+  if (!WIDE && row < V) {
     const float* r = W + (wsl * V + row) * (long long)M;
     float acc = 0.0f;
 #pragma unroll 4
@@ -2635,8 +2675,16 @@ int run_impl(int variant, const yuma_params_t* prm, int N, int E, int V, int M, 
       // shared inputs: one row-sum pass per input epoch, stored for all N
       const long long rs_in = wsh ? c1 - c0 : ns, rs_s0 = wsh ? c0 : s0;
       const int fan = wsh ? N : 1;
+      const int nchunks = (M + 255) / 256;
+      const bool wide = nchunks >= yk::kWideChunks && nchunks <= yk::kMaxWideChunks;
       tm.mark(YUMA_PHASE_ROWSUM);
-      if (vec)
+      if (wide && vec)
+        YK_LAUNCH((yk::k_rowsum<true, true>), rs_in * V, 256, st, W, S, V, M, rs_s0, V, ws.rsd,
+                  ws.sn, 0, ws.sx, fan);
+      else if (wide)
+        YK_LAUNCH((yk::k_rowsum<false, true>), rs_in * V, 256, st, W, S, V, M, rs_s0, V, ws.rsd,
+                  ws.sn, 0, ws.sx, fan);
+      else if (vec)
         YK_LAUNCH(yk::k_rowsum<true>, rs_in * rowblocks4, 256, st, W, S, V, M, rs_s0, rowblocks4,
                   ws.rsd, ws.sn, 0, ws.sx, fan);
       else
