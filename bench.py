@@ -458,8 +458,8 @@ def bench_wide(args, world: int, rank: int, dist: bool) -> dict:
     elapsed = timed(step, args.warmup, args.steps, dist, dev)
     value = float(E) * args.steps / elapsed  # one subnet: total work fixed
     per_gpu_bytes = contract_bytes(V, len(cols), variant) * E * args.steps / elapsed / 1e9
-    workload = {"workload": f"c4: wide subnet {V}V x {M}M x {E} epochs, {args.version}, miner columns "
-                            f"sharded x{world}", "V": V, "M": M, "epochs": E, "scenarios_per_gpu": 1,
+    layout = f"miner columns sharded x{world}" if dist else "unsharded, one GPU"
+    workload = {"workload": f"c4: wide subnet {V}V x {M}M x {E} epochs, {args.version}, {layout}", "V": V, "M": M, "epochs": E, "scenarios_per_gpu": 1,
                 "version": args.version, "bond_history": hist,
                 "parallelism": (f"miner-column sharded x{world} (all-gather of per-shard partials)" if dist
                                 else "single GPU, unsharded engine")}

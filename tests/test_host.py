@@ -144,6 +144,52 @@ def test_reset_index_follows_python_indexing():
                            reset_epoch=3, reset_index=-1)
 
 
+def test_reset_packing_equals_reference_statement():
+    """the packed reset against the reference's own statements run
+    in torch (simulation_utils.py:63-64 Yuma 3.1, :68-74 / :79-85 Yuma 3.2 / 4
+    with scw all zero so the condition holds wherever it is defined): for
+    every epoch of the run, which columns are zeroed, or the error raised.
+    Covers float / bool / numpy epochs and bool / numpy indices."""
+    M, E = 5, 6
+
+    def reference(mode, e_ref, idx):
+        out = {}
+        for epoch in range(1, E):  # B_state exists from epoch 1 on
+            if not epoch == e_ref:
+                continue
+            B = torch.ones(2, M)
+            if mode == engine.RESET_IF_ZERO_CONSENSUS:
+                try:
+                    fire = bool(torch.zeros(M)[idx] == 0.0)
+                except RuntimeError:
+                    return "raise"
+                if not fire:
+                    continue
+            B[:, idx] = 0.0
+            cols = frozenset(int(c) for c in (B[0] == 0).nonzero().flatten())
+            if cols:
+                out[epoch] = cols
+        return out
+
+    def packed(mode, e_ref, idx):
+        try:
+            p = engine.make_params(engine.VARIANT_YUMA3, Y.YumaConfig(), reset_mode=mode, reset_epoch=e_ref,
+                                   reset_index=idx, n_miners=M, n_epochs=E)
+        except RuntimeError:
+            return "raise"
+        if p.reset_mode == engine.RESET_NONE:
+            return {}
+        cols = range(M) if p.flags & engine.FLAG_RESET_ALL_COLUMNS else [p.reset_index]
+        return {p.reset_epoch: frozenset(cols)}
+
+    epochs = [3, 3.0, 3.5, True, False, np.int64(2), 0, -1, 6, "3", None]
+    indices = [2, -1, np.int64(4), True, False, None]
+    for mode in (engine.RESET_ALWAYS, engine.RESET_IF_ZERO_CONSENSUS):
+        for e_ref in epochs:
+            for idx in indices:
+                assert packed(mode, e_ref, idx) == reference(mode, e_ref, idx), (mode, e_ref, idx)
+
+
 def test_shard_params_keeps_all_columns_reset():
     p = engine.make_params(engine.VARIANT_YUMA3, Y.YumaConfig(), reset_mode=engine.RESET_ALWAYS,
                            reset_epoch=3, reset_index=None, n_miners=300, n_epochs=8)

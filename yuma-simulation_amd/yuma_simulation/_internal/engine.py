@@ -16,6 +16,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import numbers
 import operator
 import os
 import threading
@@ -259,17 +260,35 @@ def make_params(variant: int, config, *, maxint: int = 2**64 - 1, reset_mode: in
     return p
 
 
+def _reset_epoch_value(reset_epoch) -> int | None:
+    """The int epoch e at which the reference's `epoch == case.reset_bonds_epoch`
+    (simulation_utils.py:63,70,81; epoch an int from range()) holds, or None
+    when it never does: ints and bools (True == 1) as themselves, a float only
+    when integral (20.0 == 20, 20.5 never), anything else never."""
+    if isinstance(reset_epoch, (bool, np.bool_, numbers.Integral)):
+        return int(reset_epoch)
+    if isinstance(reset_epoch, numbers.Real):
+        f = float(reset_epoch)
+        return int(f) if f.is_integer() else None
+    return None
+
+
 def _pack_reset(p: YumaParamsC, reset_mode: int, reset_epoch, reset_index, n_miners, n_epochs) -> None:
     """The bond reset of run_simulation (simulation_utils.py:62-88) with the
     reference's Python indexing: `B_state[:, idx] = 0.0` and
     `server_consensus_weight[idx] == 0.0`, evaluated only at
     `epoch == reset_bonds_epoch` once B_state exists (epoch >= 1).
 
-    - reset_epoch None: `epoch == None` is never true, no reset;
+    - reset_epoch None or a non-integral number: never equal, no reset;
+      epochs below 1 are never reached (B_state is None at epoch 0);
     - negative index: counts from the end (idx % M);
-    - index None: `B_state[:, None]` zeroes every column (Yuma 3.1); Yuma 3.2/4
-      also evaluate `scw[None] == 0.0`, a [1, M] tensor whose truth value
-      raises RuntimeError for M > 1 (for M == 1 it is column 0);
+    - index None or True: `B_state[:, None]` / `B_state[:, True]` zeroes every
+      column (Yuma 3.1); Yuma 3.2/4 also evaluate `scw[idx] == 0.0`, a [1, M]
+      tensor whose truth value raises RuntimeError for M > 1 (for M == 1 it is
+      column 0);
+    - index False: `B_state[:, False]` selects nothing (Yuma 3.1: no reset);
+      Yuma 3.2/4's `scw[False] == 0.0` is an empty tensor whose truth value
+      raises RuntimeError;
     - index outside [-M, M): IndexError.
     The errors are raised only when the reference would reach the statement
     (reset_epoch in [1, n_epochs)). n_miners is needed for anything but a
@@ -279,18 +298,22 @@ def _pack_reset(p: YumaParamsC, reset_mode: int, reset_epoch, reset_index, n_min
     p.reset_index = 0
     if reset_mode == RESET_NONE or reset_epoch is None:
         return
-    epoch = int(reset_epoch)
-    reached = epoch >= 1 and (n_epochs is None or epoch < n_epochs)
-    if not reached and n_epochs is not None:
+    epoch = _reset_epoch_value(reset_epoch)
+    if epoch is None or epoch < 1 or (n_epochs is not None and epoch >= n_epochs):
         return  # the statement never runs
     if not -2**31 <= epoch < 2**31:
         return  # beyond any int32 epoch count: never equal
-    if reset_index is None:
+    if isinstance(reset_index, (bool, np.bool_)) and not reset_index:
+        if reset_mode == RESET_IF_ZERO_CONSENSUS:
+            raise RuntimeError("Boolean value of Tensor with no values is ambiguous "
+                               "(server_consensus_weight[False] == 0.0, simulation_utils.py:72,83)")
+        return  # B_state[:, False] = 0.0 touches nothing
+    if reset_index is None or isinstance(reset_index, (bool, np.bool_)):
         if n_miners is None:
             raise ValueError("a reset with reset_bonds_index None needs n_miners")
         if reset_mode == RESET_IF_ZERO_CONSENSUS and n_miners > 1:
             raise RuntimeError("Boolean value of Tensor with more than one value is ambiguous "
-                               "(server_consensus_weight[None] == 0.0, simulation_utils.py:72,83)")
+                               f"(server_consensus_weight[{reset_index}] == 0.0, simulation_utils.py:72,83)")
         if reset_mode == RESET_ALWAYS:
             p.flags |= FLAG_RESET_ALL_COLUMNS
             idx = 0
