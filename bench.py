@@ -24,7 +24,7 @@ Prints ONE JSON line (rank 0) with the driver's fields plus
                 BYTES(V,M) (the fp32 epoch-step contract, 12,617,728 B at
                 256 x 4096), frac = achieved / 8 TB/s; traffic = the rocprofv3
                 FETCH_SIZE + WRITE_SIZE bytes of one step (committed PMC passes of
-                this exact workload, profiles/r02/pmc_traffic.json), and
+                this exact workload, profiles/r03/pmc_traffic.json), and
                 roofline.kernel = the dominant kernel (k_bonds_elem at c2):
                 algorithmic bytes per launch / its HIP-event launch time;
   cpu_baseline  the torch-CPU restatement of the epoch (oracle/torch_cpu.py,
@@ -58,19 +58,24 @@ METRIC = "scenario-epochs/sec (256V x 4096M) at 1/8 GPUs; % of HBM peak GB/s"
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 
 
-def phase_bytes(phase: str, V: int, M: int, variant: int, liquid: bool, hist: bool, chunk: int) -> float:
+def phase_bytes(phase: str, V: int, M: int, variant: int, liquid: bool, hist: bool, chunk: int,
+                wshare: int = 1) -> float:
     """Algorithmic HBM bytes one phase must move per scenario-epoch (each input
-    read once, each output written once). DESIGN.md §Roofline tabulates them."""
+    read once, each output written once). DESIGN.md §Roofline tabulates them.
+    wshare: scenarios reading one shared input trajectory (the c3 sweep): W
+    and the per-epoch row sums are read once per input epoch for all of them,
+    so their bytes are divided among the wshare scenarios."""
     tiles = (M + 63) // 64
     VM = V * M
     colnorm = variant <= 2
+    w = 4 * VM / wshare
     table = {
-        "rowsum": 4 * VM + 4 * V + 8 * V,
-        "consensus": 4 * VM + 8 * V + 8 * M,
+        "rowsum": w + (4 * V + 8 * V) / wshare,
+        "consensus": w + 8 * V + 8 * M,
         "quantise": 8 * M + 8 * M + (4 * M if liquid else 0),
-        "rank": 4 * VM + 8 * V + 4 * M + 4 * M + 4 * tiles,
+        "rank": w + 8 * V + 4 * M + 4 * M + 4 * tiles,
         "incentive": 4 * M + 4 * tiles + 4 * M,
-        "bonds": (4 * VM + 8 * V + 4 * M + (4 * M if colnorm else 0) + (4 * M if liquid else 0)
+        "bonds": (w + 8 * V + 4 * M + (4 * M if colnorm else 0) + (4 * M if liquid else 0)
                   + (4 * VM if hist else 0) + 4 * V * tiles + 8 * VM / max(chunk, 1)),
         "finalize": 4 * V * tiles + 4 * V + 4 * V,
     }
@@ -90,7 +95,7 @@ def kernel_of(phase: str, variant: int) -> str:
     return PHASE_KERNELS[phase]
 
 
-TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r02", "pmc_traffic.json")
+TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r03", "pmc_traffic.json")
 
 
 def load_traffic(key: dict) -> dict | None:
@@ -142,9 +147,12 @@ def host_cpu() -> dict:
     usable = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else total
     threads = usable
     omp = os.environ.get("OMP_NUM_THREADS", "")
-    if omp.isdigit() and int(omp) > 0:
-        threads = min(threads, int(omp))
-    return {"model": model, "cpu_count": total, "usable": usable, "threads": threads}
+    share = "every usable CPU"
+    if omp.isdigit() and int(omp) > 0 and int(omp) < usable:
+        threads = int(omp)
+        share = (f"this process's CPU share: the GPU scheduler grants each GPU OMP_NUM_THREADS={omp} of the "
+                 f"host's {usable} usable CPUs (os.cpu_count() counts the whole host)")
+    return {"model": model, "cpu_count": total, "usable": usable, "threads": threads, "share": share}
 
 
 def cpu_baseline(variant: str, W_dev, S_dev, cfgs: list, seconds: float, warmup: int, structured_epochs: int,
@@ -195,7 +203,7 @@ def cpu_baseline(variant: str, W_dev, S_dev, cfgs: list, seconds: float, warmup:
         "kind": "port",
         "sample": (f"{label}: oracle/torch_cpu.py vectorised, {warmup} warm-up + {vn} timed epochs x {n_sc} "
                    f"scenario(s) cycling the first {ring} resident epochs ({vdt:.1f} s), torch {host['threads']} "
-                   f"threads on {host['model']} (os.cpu_count() = {host['cpu_count']}, {host['usable']} usable); "
+                   f"threads on {host['model']} ({host['share']}); "
                    f"bit-identical to the reference goldens (tests/test_oracle_golden.py)"),
         "structured": None if st is None else {
             "value": round(st[0], 4), "unit": "scenario-epochs/s", "cores": 1,
@@ -320,55 +328,76 @@ def engine_line(args, variant: int, params: list, W, S, world: int, dist: bool, 
         graph.close()
     eff_chunk = chunk if 0 < chunk <= E else E
     launches = -(-E // eff_chunk)  # launches of each phase kernel per step
+    wshare = N if shared else 1
     phase_info = {}
     for i, name in enumerate(engine.PHASES):
         if phases[i] <= 0:
             continue
-        b = phase_bytes(name, V, M, variant, liquid, hist, eff_chunk) * units
+        b = phase_bytes(name, V, M, variant, liquid, hist, eff_chunk, wshare) * units
         phase_info[name] = {"kernel": kernel_of(name, variant), "ms": round(float(phases[i]), 4),
                             "GBps": round(b / (phases[i] * 1e-3) / 1e9, 1)}
     dom = int(np.argmax(phases))
     dom_name = engine.PHASES[dom]
     dom_kernel = kernel_of(dom_name, variant)
-    dom_bytes = phase_bytes(dom_name, V, M, variant, liquid, hist, eff_chunk) * units / launches
+    dom_bytes = phase_bytes(dom_name, V, M, variant, liquid, hist, eff_chunk, wshare) * units / launches
     dom_ms = float(phases[dom]) / launches
     k_achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
 
     contract = contract_bytes(V, M, variant)
     per_gpu = value / world
-    achieved = per_gpu * contract / 1e9
+    equivalent = per_gpu * contract / 1e9
     key = {k: workload[k] for k in ("V", "M", "epochs", "scenarios_per_gpu", "version", "bond_history")}
     pmc = load_traffic(key)
+    traffic = None if pmc is None else round(sum(pmc.values()) * units)
     line = base_line(args, world, value, "scenario-epochs/s", elapsed, "weak", workload)
-    line["roofline"] = {
-        "bound": "hbm",
-        "achieved": round(achieved, 1),
-        "peak": HBM_PEAK_GBPS,
-        "unit": "GB/s",
-        "frac": round(achieved / HBM_PEAK_GBPS, 4),
-        "traffic": None if pmc is None else round(sum(pmc.values()) * units),
-        "definition": (f"SURVEY 8d step roofline: scenario-epochs/s per GPU x BYTES(V,M) = {contract:,.0f} B "
-                       "(read W, B, S; write B, Dn, C, I) / 8 TB/s; traffic = rocprofv3 FETCH_SIZE + WRITE_SIZE "
-                       "bytes of one step (profiles/r02/pmc_traffic.json)"),
-        "contract_bytes_per_step": contract * units,
-        "kernel": {
-            "name": dom_kernel,
-            "launches_per_step": launches,
-            "avg_ms": round(dom_ms, 4),
-            "bytes_per_launch": dom_bytes,
-            "achieved": round(k_achieved, 1),
-            "frac": round(k_achieved / HBM_PEAK_GBPS, 4),
-            "traffic": None if pmc is None or dom_kernel not in pmc else round(pmc[dom_kernel] * units / launches),
-            "timing": "HIP events on the launch stream around the kernel (yuma_run_profiled)",
-        },
+    kernel = {
+        "name": dom_kernel,
+        "launches_per_step": launches,
+        "avg_ms": round(dom_ms, 4),
+        "bytes_per_launch": dom_bytes,
+        "achieved": round(k_achieved, 1),
+        "frac": round(k_achieved / HBM_PEAK_GBPS, 4),
+        "traffic": None if pmc is None or dom_kernel not in pmc else round(pmc[dom_kernel] * units / launches),
+        "timing": "HIP events on the launch stream around the kernel (yuma_run_profiled)",
     }
-    if shared:
+    if not shared:
+        line["roofline"] = {
+            "bound": "hbm",
+            "achieved": round(equivalent, 1),
+            "peak": HBM_PEAK_GBPS,
+            "unit": "GB/s",
+            "frac": round(equivalent / HBM_PEAK_GBPS, 4),
+            "traffic": traffic,
+            "definition": (f"SURVEY 8d step roofline: scenario-epochs/s per GPU x BYTES(V,M) = {contract:,.0f} B "
+                           "(read W, B, S; write B, Dn, C, I) / 8 TB/s; traffic = rocprofv3 FETCH_SIZE + "
+                           f"WRITE_SIZE bytes of one step ({os.path.relpath(TRAFFIC_JSON, ROOT)})"),
+            "contract_bytes_per_step": contract * units,
+            "kernel": kernel,
+        }
+    else:
+        # one shared input trajectory: the contract's per-scenario W read
+        # never happens, so the roofline is the MEASURED HBM traffic of a step
+        # (PMC) over its time; the contract-equivalent rate is reported apart
         classes = consensus_classes(params)
-        line["roofline"]["note"] = (
-            "every scenario reads one shared W/S trajectory (beyond the epoch-step contract, SURVEY 8d): the "
-            "row sums run once per input epoch, the consensus search and rank once per consensus class "
-            f"(scenarios with equal kappa and precision: {classes} classes of {N}), bonds per scenario; frac and "
-            "the per-phase GBps count the contract bytes per scenario-epoch, i.e. equivalent rates, not HBM traffic")
+        step_s = elapsed / args.steps
+        achieved = None if traffic is None else traffic / step_s / 1e9
+        line["roofline"] = {
+            "bound": "hbm",
+            "achieved": None if achieved is None else round(achieved, 1),
+            "peak": HBM_PEAK_GBPS,
+            "unit": "GB/s",
+            "frac": None if achieved is None else round(achieved / HBM_PEAK_GBPS, 4),
+            "traffic": traffic,
+            "definition": ("measured HBM bytes of one step (rocprofv3 FETCH_SIZE + WRITE_SIZE, "
+                           f"{os.path.relpath(TRAFFIC_JSON, ROOT)}) / the step time / 8 TB/s; the kernel record counts "
+                           "W once per input epoch for all scenarios (each input read once)"),
+            "equivalent_GBps": round(equivalent, 1),
+            "equivalent_definition": (f"scenario-epochs/s per GPU x the per-scenario epoch-step contract "
+                                      f"{contract:,.0f} B: a rate, not traffic (every scenario reads one shared "
+                                      f"W/S trajectory; row sums once per input epoch, consensus and rank once "
+                                      f"per consensus class: {classes} classes of {N})"),
+            "kernel": kernel,
+        }
         line["config"]["consensus_classes"] = classes
     line["phases"] = phase_info
     return line
@@ -385,7 +414,11 @@ def bench_engine(args, world: int, rank: int, dist: bool) -> dict:
     variant, _ = resolve_version(args.version)
     liquid_version = args.version.endswith("liquid alpha on")
     if args.config == "c3":
-        cfgs = [sweep_config(rank * N + i) for i in range(N)]
+        # the sweep grid dealt to the ranks: N points per GPU (weak scaling;
+        # 8 GPUs x 512 = the whole 4096-point grid)
+        from yuma_simulation._internal.sharding import shard_range
+
+        cfgs = [sweep_config(g % 4096) for g in shard_range(N * world, world, rank)]
     else:
         cfgs = [YumaConfig(yuma_params=YumaParams(liquid_alpha=args.liquid or liquid_version))] * N
     params = [engine.make_params(variant, c) for c in cfgs]
@@ -516,20 +549,58 @@ def bench_sheet(args, world: int, rank: int, dist: bool) -> dict:
     line["roofline"] = {"bound": "latency", "kernel": "whole sheet (3x2 matrices: launch/host bound)",
                         "achieved": None, "peak": None, "unit": None, "frac": None, "traffic": None}
     if rank == 0 and not args.no_cpu_baseline:
-        from oracle import yuma_oracle as orc
-
-        t0 = time.perf_counter()
-        for r in runs:
-            W = torch.stack(list(r.case.weights_epochs)[: r.case.num_epochs]).numpy()
-            S = torch.stack(list(r.case.stakes_epochs)[: r.case.num_epochs]).numpy()
-            orc.run(r.yuma_version, W, S, r.yuma_config, r.case.reset_bonds_epoch, r.case.reset_bonds_index,
-                    validators=r.case.validators)
-        dt = time.perf_counter() - t0
-        line["cpu_baseline"] = {"value": round(units / dt, 1), "unit": "scenario-epochs/s", "cores": 1,
-                                "kind": "port", "sample": f"all {len(runs)} sheet runs, numpy oracle "
-                                                          f"(oracle/yuma_oracle.py), 1 thread, {dt:.1f} s",
-                                "host": host_cpu()}
+        line["cpu_baseline"] = sheet_cpu_baseline(len(runs), units)
     return line
+
+
+def _sheet_worker_init():
+    import torch as _t
+
+    _t.set_num_threads(1)
+    _sheet_chunk([0])  # warm: imports, case construction
+
+
+def _sheet_chunk(idx: list) -> float:
+    """Worker: run_simulation (oracle/torch_cpu.py, bit-identical to the
+    reference's dividend lists) for the sheet runs `idx`; returns seconds."""
+    from oracle import torch_cpu as tc
+    from yuma_simulation._internal.cases import cases
+    from yuma_simulation._internal.simulation_utils import SHEET_BOND_PENALTIES, _sheet_runs, sheet_yuma_versions
+    from yuma_simulation._internal.yumas import SimulationHyperparameters
+
+    runs = [r for b in SHEET_BOND_PENALTIES
+            for r in _sheet_runs(cases, sheet_yuma_versions(), SimulationHyperparameters(bond_penalty=b))]
+    t0 = time.perf_counter()
+    for i in idx:
+        r = runs[i]
+        c = r.case
+        tc.run_simulation(r.yuma_version, c.weights_epochs, c.stakes_epochs, r.yuma_config, c.num_epochs,
+                          c.validators, c.reset_bonds_epoch, c.reset_bonds_index)
+    return time.perf_counter() - t0
+
+
+def sheet_cpu_baseline(n_runs: int, units: int) -> dict:
+    """c5 CPU baseline: the reference's run_simulation restated in CPU torch
+    (oracle/torch_cpu.run_simulation) over all sheet runs, dealt round-robin to
+    one single-threaded worker process per CPU of this process's share (3 x 2
+    matrices: intra-op threads cannot help, independent runs can)."""
+    import multiprocessing as mp
+
+    host = host_cpu()
+    k = max(1, host["threads"])
+    chunks = [list(range(i, n_runs, k)) for i in range(k)]
+    ctx = mp.get_context("spawn")  # the parent holds a GPU context: never fork it
+    with ctx.Pool(k, initializer=_sheet_worker_init) as pool:
+        pool.map(_sheet_chunk, [[0]] * k)  # every worker started and warm
+        t0 = time.perf_counter()
+        busy = pool.map(_sheet_chunk, chunks)
+        dt = time.perf_counter() - t0
+    return {"value": round(units / dt, 1), "unit": "scenario-epochs/s", "cores": k, "kind": "port",
+            "sample": (f"all {n_runs} sheet runs ({units} scenario-epochs): oracle/torch_cpu.run_simulation "
+                       f"(bit-identical to the reference's dividend lists, tests/test_oracle_golden.py), dealt to "
+                       f"{k} single-threaded worker processes ({host['share']}); {dt:.2f} s wall, "
+                       f"{max(busy):.2f} s on the busiest worker, on {host['model']}"),
+            "host": host}
 
 
 DEFAULTS = {  # per config: epochs, validators, miners, scenarios per GPU, version, history

@@ -241,12 +241,16 @@ int yuma_epoch(int variant, const yuma_params_t* params_dev, int N, int V, int M
  *   stage 4 <- rsum [E][N]; levels_all [E][N][M_total] (liquid scenarios)
  *           -> dsum_part   [E][N][V] = sum over local columns of B * I
  *   stage 5 <- dsum [E][N][V]; writes Dn / D
+ * validator_trust (out->Tv, yumas.py:224 `W_clipped.sum(1) / W.sum(1)`):
+ *   stage 3 -> tv_part [2][E][N][V] = sums over local columns of Wc and Wn
+ *   stage 5 <- tv      [2][E][N][V] = sum over shards of tv_part; Tv = tv[0] / tv[1]
+ *   (the workspace must then be sized with full_outputs = 1)
  *
  * Every stage takes the same arguments as yuma_run (W [E][N][V][M] holds the
  * local columns; outputs are the local columns of the [..][M] outputs) and
  * the same workspace, which carries state from stage to stage. params must
  * carry reset_index relative to col0 (reset_mode NONE on shards that do not
- * own the reset column). validator_trust (out->Tv) is not produced.
+ * own the reset column).
  * ---------------------------------------------------------------------- */
 typedef struct yuma_shard_io {
   int M_total;             /* global miner count                              */
@@ -263,6 +267,8 @@ typedef struct yuma_shard_io {
   const int* levels_all;   /* stage 4 in, required when a scenario is liquid  */
   float* dsum_part;        /* stage 4 out                                     */
   const float* dsum;       /* stage 5 in                                      */
+  float* tv_part;          /* stage 3 out when out->Tv: [2][E][N][V]          */
+  const float* tv;         /* stage 5 in when out->Tv:  [2][E][N][V]          */
 } yuma_shard_io_t;
 
 int yuma_shard_stage(int stage, int variant, const yuma_params_t* params_dev, int N, int E,

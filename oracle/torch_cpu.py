@@ -1,5 +1,6 @@
-"""torch-CPU restatement of the Yuma 3 / Yuma 4 epoch step -- TEST AND
-BASELINE INFRASTRUCTURE, not product code.
+"""torch-CPU restatement of the Yuma epoch step (all five variants) and of
+run_simulation's epoch loop -- TEST AND BASELINE INFRASTRUCTURE, not product
+code.
 
 Only tests/ and bench.py's cpu_baseline leg import this module (SURVEY §8d:
 "time the build's CPU restatement ... (i) reference-structured, (ii)
@@ -73,7 +74,8 @@ def consensus_vectorised(W: torch.Tensor, S: torch.Tensor, kappa: float, precisi
 
 
 def _liquid_bond_alpha(C: torch.Tensor, cfg):
-    """yumas.py:546-568 (Yuma4's copy of the liquid-alpha block)."""
+    """The liquid-alpha block every variant but Yuma3 carries (yumas.py:118-140,
+    :231-253, :345-367, :546-568). Returns (bond_alpha, a, b)."""
     high = cfg.override_consensus_high if cfg.override_consensus_high is not None else C.quantile(0.75)
     low = cfg.override_consensus_low if cfg.override_consensus_low is not None else C.quantile(0.25)
     if high == low:
@@ -86,24 +88,62 @@ def _liquid_bond_alpha(C: torch.Tensor, cfg):
     return 1 - torch.clamp(alpha, cfg.alpha_low, cfg.alpha_high), a, b
 
 
+VARIANTS = ("rust", "yuma1", "yuma2", "yuma3", "yuma4")
+
+
 def epoch(variant: str, W: torch.Tensor, S: torch.Tensor, B_old: torch.Tensor | None, cfg,
-          consensus: str = "structured", maxint: int = 2**64 - 1) -> dict:
-    """One Yuma3 (yumas.py:399-491) or Yuma4 (:494-606) call on CPU tensors."""
-    if variant not in ("yuma3", "yuma4"):
-        raise ValueError(f"torch_cpu restates yuma3 / yuma4, not {variant}")
+          consensus: str = "structured", maxint: int = 2**64 - 1, W_prev: torch.Tensor | None = None) -> dict:
+    """One YumaRust (yumas.py:61-172), Yuma (:175-282), Yuma2 (:285-396),
+    Yuma3 (:399-491) or Yuma4 (:494-606) call on CPU tensors, returning the
+    reference's result dict (same keys, dtypes and Python-float entries)."""
+    if variant not in VARIANTS:
+        raise ValueError(f"torch_cpu restates {VARIANTS}, not {variant}")
     Wn = (W.T / (W.sum(dim=1) + 1e-6)).T
+    if variant == "yuma2" and W_prev is None:
+        W_prev = Wn
     Sn = S / S.sum()
     P = (Sn.view(-1, 1) * Wn).sum(dim=0)
     find = consensus_structured if consensus == "structured" else consensus_vectorised
     C = find(Wn, Sn, cfg.kappa, cfg.consensus_precision)
+    if variant == "rust":  # C is an fp64 tensor there (yumas.py:81); the bisection points are exact
+        C = C.to(torch.float64)
     C = (C / C.sum() * 65_535).int() / 65_535
-    Wc = torch.min(Wn, C)
+    Wc = torch.min(W_prev if variant == "yuma2" else Wn, C)
     R = (Sn.view(-1, 1) * Wc).sum(dim=0)
     I = (R / R.sum()).nan_to_num(0)
     T = (R / P).nan_to_num(0)
     Tv = Wc.sum(dim=1) / Wn.sum(dim=1)
     out = {"weight": Wn, "stake": Sn, "server_prerank": P, "server_consensus_weight": C,
            "consensus_clipped_weight": Wc, "server_rank": R, "server_incentive": I}
+    if variant in ("rust", "yuma1", "yuma2"):
+        if variant == "rust":
+            B = Sn.view(-1, 1) * Wc
+            B = B / (B.sum(dim=0) + 1e-6)
+            B = torch.nan_to_num(B)
+        else:
+            Wb = (1 - cfg.bond_penalty) * (W_prev if variant == "yuma2" else Wn) + cfg.bond_penalty * Wc
+            B = Sn.view(-1, 1) * Wb / (Sn.view(-1, 1) * Wb).sum(dim=0)
+            B = B.nan_to_num(0)
+        a = b = torch.tensor(float("nan"))
+        ba = cfg.bond_alpha
+        if cfg.liquid_alpha:
+            ba, a, b = _liquid_bond_alpha(C, cfg)
+        if B_old is not None:
+            Bema = ba * B + (1 - ba) * B_old
+        else:
+            Bema = B.clone() if variant == "rust" else B
+        if variant == "rust":
+            Bema = Bema / (Bema.sum(dim=0) + 1e-6)
+            Bema = torch.nan_to_num(Bema)
+        D = (Bema * I).sum(dim=1)
+        out.update(server_trust=T, validator_trust=Tv)
+        if variant != "rust":
+            out["weight_for_bond"] = Wb
+        out.update(validator_bond=B, validator_ema_bond=Bema)
+        out["validator_reward"] = D
+        out["validator_reward_normalized"] = D / (D.sum() + 1e-6)
+        out.update(bond_alpha=ba, alpha_a=a, alpha_b=b)
+        return out
     Bo = torch.zeros_like(Wn) if B_old is None else B_old
     if variant == "yuma3":
         cap = Sn.unsqueeze(1) * maxint
@@ -126,6 +166,10 @@ def epoch(variant: str, W: torch.Tensor, S: torch.Tensor, B_old: torch.Tensor | 
     return out
 
 
+def state_key(variant: str) -> str:
+    return "validator_bonds" if variant in ("yuma3", "yuma4") else "validator_ema_bond"
+
+
 def run(variant: str, W_epochs: torch.Tensor, S_epochs: torch.Tensor, cfg, consensus: str = "structured",
         epochs: int | None = None) -> dict:
     """The run_simulation loop (simulation_utils.py:52-110) without resets,
@@ -138,3 +182,49 @@ def run(variant: str, W_epochs: torch.Tensor, S_epochs: torch.Tensor, cfg, conse
         Dn.append(r["validator_reward_normalized"])
         C.append(r["server_consensus_weight"])
     return {"Dn": torch.stack(Dn), "C": torch.stack(C), "B": B}
+
+
+# version string -> (variant, reset rule) of run_simulation's dispatch (simulation_utils.py:52-93)
+VERSIONS = {
+    "Yuma 0 (subtensor)": ("rust", None),
+    "Yuma 1 (paper)": ("yuma1", None),
+    "Yuma 1 (paper) - liquid alpha on": ("yuma1", None),
+    "Yuma 2 (Adrian-Fish)": ("yuma2", None),
+    "Yuma 3 (Rhef)": ("yuma3", None),
+    "Yuma 3.1 (Rhef+reset)": ("yuma3", "always"),
+    "Yuma 3.2 (Rhef+conditional)": ("yuma3", "if_zero"),
+    "Yuma 4 (Rhef+relative bonds)": ("yuma4", "if_zero"),
+    "Yuma 4 (Rhef+relative bonds) - liquid alpha on": ("yuma4", "if_zero"),
+}
+
+
+def run_simulation(version: str, weights_epochs, stakes_epochs, cfg, num_epochs: int, validators,
+                   reset_bonds_epoch=None, reset_bonds_index=None, consensus: str = "structured"):
+    """run_simulation (simulation_utils.py:26-112) on CPU torch: the epoch
+    loop with the bond resets and the fp64 dividend-per-1000-tao lists.
+    Returns (dividends_per_validator, bonds_per_epoch, incentives_per_epoch)."""
+    if version not in VERSIONS:
+        raise ValueError("Invalid Yuma function.")
+    variant, reset = VERSIONS[version]
+    div = {v: [] for v in validators}
+    bonds, incentives = [], []
+    B_state = W_prev = scw = None
+    for epoch_i in range(num_epochs):
+        W, S = weights_epochs[epoch_i], stakes_epochs[epoch_i]
+        units = S * cfg.total_subnet_stake / 1000.0
+        if reset is not None and B_state is not None and epoch_i == reset_bonds_epoch:
+            if reset == "always" or (scw is not None and scw[reset_bonds_index] == 0.0):
+                B_state[:, reset_bonds_index] = 0.0
+        r = epoch(variant, W, S, B_state, cfg, consensus, W_prev=W_prev)
+        B_state = r[state_key(variant)]
+        if variant == "yuma2":
+            W_prev = r["weight"]
+        scw = r["server_consensus_weight"]
+        emis = cfg.validator_emission_ratio * r["validator_reward_normalized"] * cfg.total_epoch_emission
+        for i, v in enumerate(validators):
+            su = float(units[i].item())
+            ei = float(emis[i].item())
+            div[v].append(ei / su if su > 1e-6 else 0.0)
+        bonds.append(B_state.clone())
+        incentives.append(r["server_incentive"])
+    return div, bonds, incentives

@@ -1,7 +1,10 @@
-"""Multi-process scenario sharding over torch.distributed (gloo, world_size 2,
-CPU). The engine itself needs a GPU, so the ranks use a CPU stand-in runner
-built on the oracle; what is tested is the distribution logic: shard
-boundaries, per-rank parameter selection, and the rank-ordered gather."""
+"""Multi-process scenario sharding over torch.distributed (gloo, world_size 2).
+
+CPU tests: the ranks use a CPU stand-in runner built on the oracle; what is
+tested is the distribution logic (shard boundaries, per-rank parameter
+selection, the rank-ordered gather). GPU tests: the same
+two ranks run the HIP engine (two processes sharing one GPU), replicated and
+shared-input (c3) sweeps, bitwise against the one-process run."""
 
 import os
 import socket
@@ -94,3 +97,62 @@ def test_shard_range_partitions():
             assert max(sizes) - min(sizes) <= 1
     with pytest.raises(ValueError):
         shard_range(4, 2, 2)
+
+
+# ---------------------------------------------------------------------------
+# GPU: the engine inside the ranks
+# ---------------------------------------------------------------------------
+GE, GV, GM = 6, 64, 512
+
+
+def _engine_worker(rank, world, port, n_total, shared, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from yuma_simulation._internal import engine
+
+        params = [engine.make_params(engine.VARIANT_YUMA4, c) for c in configs(n_total)]
+        mine = shard_range(n_total, world, rank)
+        W = engine.synth_weights(11, GE, 1 if shared else n_total, GV, GM)
+        S = torch.from_numpy(synth.stakes(11, GE, 1 if shared else n_total, GV, period=2)).to(W.device)
+        if not shared:
+            W, S = W[:, mine.start:mine.stop].contiguous(), S[:, mine.start:mine.stop].contiguous()
+        res = run_sharded(engine.VARIANT_YUMA4, params, W, S, n_total=n_total, shared_inputs=shared)
+        torch.cuda.synchronize()
+        q.put((rank, res.Dn.cpu().numpy(), res.C.cpu().numpy(), res.I.cpu().numpy(),
+               res.B_final.cpu().numpy(), list(res.local)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n_total,shared", [(5, False), (6, True)])
+def test_engine_scenario_sharding_gloo_world2(n_total, shared):
+    """run_sharded -> engine.run in each of two ranks (one GPU, two
+    processes): every rank holds all scenarios' Dn / C / I after the gather
+    and its own B_final, all bitwise equal to one engine call over every
+    scenario in this process."""
+    from yuma_simulation._internal import engine
+
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_engine_worker, args=(r, world, port, n_total, shared, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    params = [engine.make_params(engine.VARIANT_YUMA4, c) for c in configs(n_total)]
+    W = engine.synth_weights(11, GE, 1 if shared else n_total, GV, GM)
+    S = torch.from_numpy(synth.stakes(11, GE, 1 if shared else n_total, GV, period=2)).to(W.device)
+    full = engine.run(engine.VARIANT_YUMA4, params, W, S, shared_inputs=shared)
+    torch.cuda.synchronize()
+    for rank, Dn, C, I, Bf, local in got:
+        assert local == list(shard_range(n_total, world, rank))
+        np.testing.assert_array_equal(Dn, full.Dn.cpu().numpy())
+        np.testing.assert_array_equal(C, full.C.cpu().numpy())
+        np.testing.assert_array_equal(I, full.I.cpu().numpy())
+        np.testing.assert_array_equal(Bf, full.B_final[local[0]:local[-1] + 1].cpu().numpy())

@@ -68,7 +68,9 @@ def _gather_worker(rank, world, port, q):
     try:
         g = wide.dist_gather()
         x = torch.arange(6 * (rank + 2), dtype=torch.float32).reshape(2, 3, rank + 2) + 100 * rank
-        parts = g([x])
+        parts = g([x], [2, 3])
+        same = g([torch.full((2, 2), float(rank))])
+        assert [float(p[0, 0]) for p in same] == [0.0, 1.0]
         tot = wide.ordered_sum([torch.ones(4) * (r + 1) for r in range(world)])
         q.put((rank, [p.numpy() for p in parts], tot.numpy()))
     finally:
@@ -154,6 +156,31 @@ def test_wide_local_matches_unsharded(name, n_shards):
     got = wide.run_wide_local(variant, params, W, S, n_shards, want_hist=True)
     torch.cuda.synchronize()
     _compare(got, ref, wide.column_ranges(M, n_shards))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["rust", "yuma2", "yuma3"])
+@pytest.mark.parametrize("n_shards", [1, 3])
+def test_wide_local_validator_trust(name, n_shards):
+    """validator_trust (yumas.py:224, `W_clipped.sum(1) /
+    W.sum(1)`) from miner-column shards: stage 3 sums Wc and Wn over each
+    shard's tiles, the totals are added in shard order. One shard adds the
+    tiles exactly as the unsharded finalize (bitwise); three shards
+    re-associate the sum (within 1e-5)."""
+    variant, par = CASES[name]
+    W, S = _inputs(0x5EED47)
+    params = _params(variant, par, W.shape[1])
+    ref = engine.run(variant, params, W, S, want_hist=True, want=("Tv",))
+    got = wide.run_wide_local(variant, params, W, S, n_shards, want_hist=True, want=("Tv",))
+    torch.cuda.synchronize()
+    _compare(got, ref, wide.column_ranges(M, n_shards))
+    tv = got.extra["Tv"][0]
+    if n_shards == 1:
+        assert torch.equal(tv, ref.extra["Tv"])
+    else:
+        for t in got.extra["Tv"][1:]:
+            assert torch.equal(t, tv)  # every shard holds the same totals
+        assert_close(tv.cpu().numpy(), ref.extra["Tv"].cpu().numpy(), what="Tv")
 
 
 @pytest.mark.gpu

@@ -1,4 +1,4 @@
-"""Turn rocprofv3 PMC passes into per-kernel HBM bytes (profiles/r02/pmc_traffic.json,
+"""Turn rocprofv3 PMC passes into per-kernel HBM bytes (profiles/r03/pmc_traffic.json,
 one record per bench workload; bench.py reads roofline.traffic from it).
 
 Two separate counter passes of the same bench command (MI355X_MICROARCH.md
@@ -64,7 +64,7 @@ def main():
     ap.add_argument("--M", type=int, default=4096)
     ap.add_argument("--version", default="Yuma 3 (Rhef)")
     ap.add_argument("--history", action="store_true")
-    ap.add_argument("--out", default=os.path.join(os.path.dirname(__file__), "..", "profiles", "r02",
+    ap.add_argument("--out", default=os.path.join(os.path.dirname(__file__), "..", "profiles", "r03",
                                                   "pmc_traffic.json"))
     ap.add_argument("--launches", type=int, default=1, help="launches of each kernel per bench step")
     a = ap.parse_args()

@@ -2793,8 +2793,11 @@ int shard_stage_impl(int stage, int variant, const yuma_params_t* prm, int N, in
   if (io->M_total < M || io->col0 < 0 || io->col0 + M > io->M_total)
     return fail(YUMA_EINVAL, "shard [%d, %d) outside M_total=%d", io->col0, io->col0 + M,
                 io->M_total);
-  if (out->Tv != nullptr) return fail(YUMA_EUNSUPPORTED, "validator_trust is not produced by shards");
-  Workspace ws = carve((char*)workspace, variant, N, E, V, M, 0);
+  // validator_trust (yumas.py:224): stage 3 sums sum(Wc) and sum(Wn) over
+  // the local columns (per-tile partials, tiles in order), stage 5 divides
+  // the shard-ordered totals the caller hands back
+  const int full = out->Tv != nullptr;
+  Workspace ws = carve((char*)workspace, variant, N, E, V, M, full);
   if (ws.bytes > ws_bytes)
     return fail(YUMA_EWORKSPACE, "workspace %zu < required %zu bytes", ws_bytes, ws.bytes);
   hipStream_t st = (hipStream_t)stream;
@@ -2843,17 +2846,22 @@ int shard_stage_impl(int stage, int variant, const yuma_params_t* prm, int N, in
     case 3: {
       if ((rust ? !io->csum_d : !io->csum) || !io->rsum_part)
         return fail(YUMA_EINVAL, "stage 3 needs io->csum%s and io->rsum_part", rust ? "_d" : "");
+      if (full && !io->tv_part) return fail(YUMA_EINVAL, "stage 3 with out->Tv needs io->tv_part");
       YK_LAUNCH(yk::k_quantise<256>, ns, 256, st, ws.craw, prm, variant, N, M, 0LL, C, qlev,
                 ba_buf, ws.scal, rust ? nullptr : io->csum, rust ? io->csum_d : nullptr, 1, nullptr);
       if (vec)
         launch_rank<true>(rc, ns * tiles, st, W, ws.rsd, ws.sn, C, Wprev_init,
                           variant == YUMA_VARIANT_YUMA2, N, V, M, 0LL, tiles, R, ws.rpart,
-                          out->Wn, out->Wc, nullptr, nullptr, 0);
+                          out->Wn, out->Wc, ws.tvc, ws.tvn, 0);
       else
         launch_rank<false>(rc, ns * tiles, st, W, ws.rsd, ws.sn, C, Wprev_init,
                            variant == YUMA_VARIANT_YUMA2, N, V, M, 0LL, tiles, R, ws.rpart,
-                           out->Wn, out->Wc, nullptr, nullptr, 0);
+                           out->Wn, out->Wc, ws.tvc, ws.tvn, 0);
       YK_LAUNCH(yk::k_rsum, ns, 64, st, ws.rpart, tiles, io->rsum_part);
+      if (full) {
+        YK_LAUNCH(yk::k_dsum, ns, 256, st, ws.tvc, V, tiles, io->tv_part);
+        YK_LAUNCH(yk::k_dsum, ns, 256, st, ws.tvn, V, tiles, io->tv_part + ns * V);
+      }
       break;
     }
     case 4: {
@@ -2900,8 +2908,10 @@ int shard_stage_impl(int stage, int variant, const yuma_params_t* prm, int N, in
     }
     case 5: {
       if (!io->dsum) return fail(YUMA_EINVAL, "stage 5 needs io->dsum");
-      YK_LAUNCH(yk::k_finalize, ns, 256, st, io->dsum, ws.sn, variant, V, 0LL, 1, nullptr,
-                nullptr, out->Dn, out->D, nullptr);
+      if (full && !io->tv) return fail(YUMA_EINVAL, "stage 5 with out->Tv needs io->tv");
+      YK_LAUNCH(yk::k_finalize, ns, 256, st, io->dsum, ws.sn, variant, V, 0LL, 1,
+                full ? io->tv : nullptr, full ? io->tv + ns * V : nullptr, out->Dn, out->D,
+                out->Tv);
       if (out->Sn != nullptr)
         (void)hipMemcpyAsync(out->Sn, ws.sn, (size_t)ns * V * 4, hipMemcpyDeviceToDevice, st);
       if (out->alpha_ab != nullptr)

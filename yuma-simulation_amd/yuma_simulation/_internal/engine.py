@@ -107,7 +107,7 @@ class YumaOutputsC(ctypes.Structure):
 
 
 SHARD_IO_FIELDS = ("rowsum_part", "rowsum", "csum_part", "csum_part_d", "csum", "csum_d",
-                   "levels", "rsum_part", "rsum", "levels_all", "dsum_part", "dsum")
+                   "levels", "rsum_part", "rsum", "levels_all", "dsum_part", "dsum", "tv_part", "tv")
 
 
 class YumaShardIOC(ctypes.Structure):

@@ -44,16 +44,20 @@ def _gather_scenarios(x: torch.Tensor, counts: list[int], group=None) -> torch.T
     pad[1] = width
     buf = torch.zeros(pad, dtype=x.dtype, device=x.device)
     buf[:, : x.shape[1]] = x
+    if dist.get_backend(group) == "gloo":  # gloo gathers through host memory
+        buf = buf.cpu()
     parts = [torch.empty_like(buf) for _ in range(world)]
-    dist.all_gather(parts, buf.contiguous(), group=group)
-    return torch.cat([p[:, :c] for p, c in zip(parts, counts)], dim=1)
+    dist.all_gather(parts, buf, group=group)
+    return torch.cat([p[:, :c] for p, c in zip(parts, counts)], dim=1).to(x.device)
 
 
 def run_sharded(variant: int, params_all: list, W_local: torch.Tensor, S_local: torch.Tensor, *,
                 n_total: int, gather: bool = True, group=None, runner=None, **run_kwargs) -> ShardedResult:
     """Run this rank's scenarios. W_local [E, n_local, V, M], S_local
     [E, n_local, V] hold exactly the scenarios of shard_range(n_total, world,
-    rank); params_all has one record per GLOBAL scenario. `runner` defaults
+    rank) — or, with shared_inputs=True (a parameter sweep over one subnet,
+    config c3), the one trajectory [E, 1, V, M] / [E, 1, V] every scenario
+    reads; params_all has one record per GLOBAL scenario. `runner` defaults
     to engine.run (tests pass a CPU stand-in with the same signature)."""
     if runner is None:
         from yuma_simulation._internal import engine
@@ -62,7 +66,8 @@ def run_sharded(variant: int, params_all: list, W_local: torch.Tensor, S_local: 
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     rank = dist.get_rank(group) if dist.is_initialized() else 0
     mine = shard_range(n_total, world, rank)
-    if W_local.shape[1] != len(mine) or S_local.shape[1] != len(mine):
+    n_in = 1 if run_kwargs.get("shared_inputs") else len(mine)
+    if W_local.shape[1] != n_in or S_local.shape[1] != n_in:
         raise ValueError(f"rank {rank} holds {W_local.shape[1]} scenarios, shard is {len(mine)}")
     res = runner(variant, [params_all[i] for i in mine], W_local, S_local, **run_kwargs)
     Dn, C, I = res.Dn, res.C, res.I

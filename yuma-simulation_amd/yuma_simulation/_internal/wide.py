@@ -14,7 +14,11 @@ partials are all-gathered (RCCL over xGMI; gloo on CPU) and summed in shard
 order, so every rank sees bit-identical totals and the result does not
 depend on timing. Four small exchanges per run, independent of E:
 [E,N,V] row sums, [E,N] sum C, [E,N] sum R (+ the [E,N,M] levels when a
-scenario uses liquid alpha), [E,N,V] dividend partials.
+scenario uses liquid alpha), [E,N,V] dividend partials (+ the [2,E,N,V] sums
+of Wc and Wn when validator_trust, yumas.py:224, is requested). The level
+exchange is SURVEY §8e's "all-gather of C" option (the quantised C as int32
+levels, M_total x 4 B per slice): the same bytes as a 65536-bin histogram and
+one exchange instead of a two-pass radix select.
 
 The same orchestration drives several shards inside ONE process
 (`run_wide_local`); `run_wide_distributed` is the one-shard-per-rank form.
@@ -99,11 +103,15 @@ class WideResult:
     extra: dict
 
 
-Gather = Callable[[list[torch.Tensor]], list[torch.Tensor]]
+# gather(list of this process's per-shard tensors, widths) -> every shard's
+# tensor in global shard order. widths: None when every shard's tensor has the
+# same shape, else the last-dimension size of each global shard (known from
+# column_ranges, so no size exchange is needed).
+Gather = Callable[..., list[torch.Tensor]]
 
 
 def _run_shards(variant: int, params: list, W_shards: list[torch.Tensor], S: torch.Tensor,
-                cols: list[range], M_total: int, gather: Gather, *,
+                cols: list[range], M_total: int, gather: Gather, all_cols: list[range], *,
                 B_init: list[torch.Tensor] | None = None,
                 Wprev_init: list[torch.Tensor] | None = None,
                 want_hist: bool = False, want: tuple[str, ...] = ()) -> WideResult:
@@ -128,13 +136,13 @@ def _run_shards(variant: int, params: list, W_shards: list[torch.Tensor], S: tor
         if W.shape[:3] != (E, N, V) or M != len(cols[i]):
             raise ValueError(f"shard {i}: W {tuple(W.shape)} does not match columns {cols[i]}")
         prm = engine.params_tensor(shard_params(params, cols[i]), dev)
-        ws = torch.empty(max(engine.workspace_bytes(variant, N, E, V, M, False), 1),
+        ws = torch.empty(max(engine.workspace_bytes(variant, N, E, V, M, "Tv" in want), 1),
                          dtype=torch.uint8, device=dev)
         out = {"Dn": torch.empty(E, N, V, **f32), "C": torch.empty(E, N, M, **f32),
                "I": torch.empty(E, N, M, **f32), "B_final": torch.empty(N, V, M, **f32)}
         if want_hist:
             out["B_hist"] = torch.empty(E, N, V, M, **f32)
-        shapes = {"D": (E, N, V), "R": (E, N, M), "P": (E, N, M), "T": (E, N, M),
+        shapes = {"D": (E, N, V), "R": (E, N, M), "P": (E, N, M), "T": (E, N, M), "Tv": (E, N, V),
                   "Sn": (E, N, V), "bond_alpha": (E, N, M), "alpha_ab": (E, N, 2)}
         for name in want:
             if name not in shapes:
@@ -146,6 +154,8 @@ def _run_shards(variant: int, params: list, W_shards: list[torch.Tensor], S: tor
               "levels": torch.empty(E, N, M, dtype=torch.int32, device=dev),
               "rsum_part": torch.empty(E, N, **f32),
               "dsum_part": torch.empty(E, N, V, **f32)}
+        if "Tv" in want:
+            io["tv_part"] = torch.empty(2, E, N, V, **f32)
         if rust:
             io["csum_part_d"] = torch.empty(E, N, dtype=torch.float64, device=dev)
         else:
@@ -161,7 +171,7 @@ def _run_shards(variant: int, params: list, W_shards: list[torch.Tensor], S: tor
                                workspace=s["ws"])
 
     def reduce(name: str) -> torch.Tensor:
-        return ordered_sum(gather([s["io"][name] for s in sh]))
+        return ordered_sum(gather([s["io"][name] for s in sh], None))
 
     stage(1)
     rowsum = reduce("rowsum_part")
@@ -178,11 +188,15 @@ def _run_shards(variant: int, params: list, W_shards: list[torch.Tensor], S: tor
             s["io"]["csum"] = csum
     stage(3)
     rsum = reduce("rsum_part")
+    tv = reduce("tv_part") if "Tv" in want else None
     levels_all = None
     if liquid:
-        levels_all = torch.cat(gather([s["io"]["levels"] for s in sh]), dim=2).contiguous()
+        widths = [len(c) for c in all_cols]
+        levels_all = torch.cat(gather([s["io"]["levels"] for s in sh], widths), dim=2).contiguous()
     for s in sh:
         s["io"]["rsum"] = rsum
+        if tv is not None:
+            s["io"]["tv"] = tv
         if levels_all is not None:
             s["io"]["levels_all"] = levels_all
     stage(4)
@@ -214,35 +228,36 @@ def run_wide_local(variant: int, params: list, W: torch.Tensor, S: torch.Tensor,
         kw["B_init"] = [B_init[..., c.start:c.stop] for c in cols]
     if Wprev is not None:
         kw["Wprev_init"] = [Wprev[..., c.start:c.stop] for c in cols]
-    return _run_shards(variant, params, W_shards, S, cols, M, lambda xs: xs, **kw)
+    return _run_shards(variant, params, W_shards, S, cols, M, lambda xs, widths=None: xs, cols, **kw)
 
 
 def dist_gather(group=None) -> Gather:
     """All-gather of one tensor per rank (RCCL over xGMI under the nccl
-    backend; through host memory under gloo), ranks in order. Tensors may
-    differ in their LAST dimension (uneven column shards)."""
+    backend; through host memory under gloo), ranks in order. Shapes are known
+    up front — equal on every rank, or differing only in the last dimension
+    by the caller's `widths` (uneven column shards) — so one collective per
+    exchange, no size exchange and no host synchronisation under nccl."""
     world = dist.get_world_size(group)
     cpu = dist.get_backend(group) == "gloo"
 
-    def gather(xs: list[torch.Tensor]) -> list[torch.Tensor]:
+    def gather(xs: list[torch.Tensor], widths: list[int] | None = None) -> list[torch.Tensor]:
         (x,) = xs
         dev = x.device
-        sizes = torch.tensor([x.shape[-1]], dtype=torch.int64)
-        all_sizes = [torch.zeros_like(sizes) for _ in range(world)]
-        if cpu:
-            dist.all_gather(all_sizes, sizes, group=group)
+        if widths is not None:
+            if len(widths) != world:
+                raise ValueError(f"{len(widths)} widths for {world} ranks")
+            width = max(widths)
+            src = torch.zeros(*x.shape[:-1], width, dtype=x.dtype, device=dev)
+            src[..., : x.shape[-1]] = x
         else:
-            sz = sizes.to(dev)
-            tmp = [torch.zeros_like(sz) for _ in range(world)]
-            dist.all_gather(tmp, sz, group=group)
-            all_sizes = [t.cpu() for t in tmp]
-        width = int(max(int(s) for s in all_sizes))
-        pad = torch.zeros(*x.shape[:-1], width, dtype=x.dtype, device=dev)
-        pad[..., : x.shape[-1]] = x
-        src = pad.cpu() if cpu else pad
+            src = x.contiguous()
+        if cpu:
+            src = src.cpu()
         parts = [torch.empty_like(src) for _ in range(world)]
-        dist.all_gather(parts, src.contiguous(), group=group)
-        return [p[..., : int(n)].to(dev) for p, n in zip(parts, all_sizes)]
+        dist.all_gather(parts, src, group=group)
+        if widths is not None:
+            parts = [p[..., :w] for p, w in zip(parts, widths)]
+        return [p.to(dev) for p in parts]
 
     return gather
 
@@ -259,4 +274,5 @@ def run_wide_distributed(variant: int, params: list, W_local: torch.Tensor, S: t
     for key in ("B_init", "Wprev_init"):
         if kw.get(key) is not None:
             kw[key] = [kw[key]]
-    return _run_shards(variant, params, [W_local], S, [cols], M_total, dist_gather(group), **kw)
+    return _run_shards(variant, params, [W_local], S, [cols], M_total, dist_gather(group),
+                       column_ranges(M_total, world), **kw)
