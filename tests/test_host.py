@@ -51,6 +51,21 @@ def test_compute_without_gpu_fails_loudly():
         Y.Yuma(torch.rand(4, 8), torch.rand(4))
 
 
+def test_engine_limits_raise_clear_errors():
+    """the engine's limits (V <= 1024, consensus_precision
+    <= 2**30; the reference has neither) surface as EngineError with the
+    limit named, before any GPU work (DESIGN.md §3 'Limits')."""
+    with pytest.raises(engine.EngineError, match="1024"):
+        Y.Yuma3(torch.rand(1025, 8), torch.rand(1025))
+    with pytest.raises(engine.EngineError, match="1024"):
+        engine.run(engine.VARIANT_YUMA4, [], torch.zeros(1, 1, 2048, 4), torch.zeros(1, 1, 2048))
+    cfg = Y.YumaConfig(simulation=Y.SimulationHyperparameters(consensus_precision=2**31))
+    with pytest.raises(engine.EngineError, match="2\\*\\*30"):
+        Y.Yuma(torch.rand(4, 8), torch.rand(4), config=cfg)
+    assert engine.make_params(engine.VARIANT_YUMA1, Y.YumaConfig(
+        simulation=Y.SimulationHyperparameters(consensus_precision=2**30))).bisect_iters == 30
+
+
 def test_config_defaults_and_flattening():
     cfg = Y.YumaConfig()
     assert (cfg.kappa, cfg.bond_penalty, cfg.total_epoch_emission) == (0.5, 1.0, 100.0)

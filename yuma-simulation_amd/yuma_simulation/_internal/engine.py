@@ -64,6 +64,21 @@ class EngineError(RuntimeError):
     """The engine rejected a call (bad sizes, workspace, launch failure)."""
 
 
+MAX_VALIDATORS = 1024  # include/yuma_hip.h YUMA_MAX_VALIDATORS (register-resident validator columns)
+MAX_BISECT_ITERS = 30  # consensus_precision <= 2**30: the search grid k / 2**iters in int32
+
+
+def check_limits(V: int, M: int) -> None:
+    """The engine's size limits, checked before anything touches a GPU. The
+    reference (yumas.py:195-209) has none; real subnets stay far inside them
+    (DESIGN.md §3 'Limits')."""
+    if V > MAX_VALIDATORS:
+        raise EngineError(f"{V} validators exceed the engine's limit of {MAX_VALIDATORS} per subnet "
+                          "(YUMA_MAX_VALIDATORS: a miner column is held in registers by one workgroup)")
+    if M > (1 << 20) * 64:
+        raise EngineError(f"{M} miners exceed the engine's limit of {(1 << 20) * 64} (2^20 tiles of 64)")
+
+
 class YumaParamsC(ctypes.Structure):
     _fields_ = [
         ("variant", ctypes.c_int32),
@@ -215,8 +230,9 @@ def make_params(variant: int, config, *, maxint: int = 2**64 - 1, reset_mode: in
     p = YumaParamsC()
     p.variant = variant
     p.bisect_iters = bisect_iterations(config.consensus_precision)
-    if p.bisect_iters > 30:
-        raise EngineError("consensus_precision above 2**30 is not supported by the engine")
+    if p.bisect_iters > MAX_BISECT_ITERS:
+        raise EngineError(f"consensus_precision {config.consensus_precision} needs {p.bisect_iters} bisection "
+                          f"steps; the engine supports at most {MAX_BISECT_ITERS} (consensus_precision <= 2**30)")
     p.kappa = f32(config.kappa)
     p.bond_penalty = f32(config.bond_penalty)
     p.one_minus_bond_penalty = f32(1 - config.bond_penalty)
@@ -373,9 +389,10 @@ def run(variant: int, params: list[YumaParamsC], W: torch.Tensor, S: torch.Tenso
     scenario (one per params record) reads — a parameter sweep over one subnet
     (yuma_run_ex, YUMA_RUN_SHARED_INPUTS); results equal a run on W and S
     replicated per scenario."""
+    E, Nw, V, M = W.shape
+    check_limits(V, M)
     dev = device()
     lib = load_library()
-    E, Nw, V, M = W.shape
     if S.shape != (E, Nw, V):
         raise ValueError(f"S shape {tuple(S.shape)} does not match W {tuple(W.shape)}")
     if shared_inputs:
