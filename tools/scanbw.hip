@@ -19,7 +19,13 @@ __global__ __launch_bounds__(BS) void k_scan(const fvec4* __restrict__ x, fvec4*
                                              int V, int M, float* out) {
   constexpr int LPR = CB / 4, G = BS / LPR;
   const int tiles = M / CB;
-  const int tile = blockIdx.x % tiles, rb = blockIdx.x / tiles;
+  int tile = blockIdx.x % tiles, rb = blockIdx.x / tiles;
+  if (DP >= 3) {  // XCD-grouped: XCD x (= block % 8) owns a contiguous band of rows, every column block
+    const int x = blockIdx.x & 7, k = blockIdx.x >> 3, per = gridDim.x >> 3;
+    const int band = per / tiles;  // row blocks per XCD
+    tile = k / band;
+    rb = x * band + k % band;
+  }
   const int c = threadIdx.x % LPR, g = threadIdx.x / LPR;
   const long long m4 = M / 4, sl = (long long)V * m4;
   long long off[R];
@@ -49,8 +55,11 @@ __global__ __launch_bounds__(BS) void k_scan(const fvec4* __restrict__ x, fvec4*
           for (int o = 1; o < 16; o <<= 1) p += __shfl_xor(p, o, 64);
           const int row = rb * G * R + g + G * i, st = (tile * CB + c * 4) / 64, tl = M / 64;
           if ((threadIdx.x & 15) == 0) {
-            if (DP == 1) out[1 + ((long long)t * tl + st) * V + row] = p;
-            else out[1 + ((long long)t * V + row) * tl + st] = p;
+            if (DP == 1 || DP == 3) out[1 + ((long long)t * tl + st) * V + row] = p;
+            else if (DP == 5) {  // [column block][V][epoch][sub-tiles of the block]
+              constexpr int TPB = CB / 64;
+              out[1 + (((long long)tile * V + row) * steps + t) * TPB + (st % TPB)] = p;
+            } else out[1 + ((long long)t * V + row) * tl + st] = p;
           }
         }
         if (t + P < steps) ring[k][i] = x[(t + P) * sl + off[i]];
@@ -104,26 +113,17 @@ int main() {
     fflush(stdout);                                                                                           \
   }
   for (int rep2 = 0; rep2 < 2; ++rep2) {
-    RUN(256, 64, 2, 2, true, 0)  // k_bonds_elem with history today
-    RUN(256, 64, 2, 2, true, 1)
+    RUN(256, 64, 2, 2, true, 1)  // k_bonds_elem with history today
+    RUN(256, 64, 2, 2, true, 5)
     RUN(512, 1024, 2, 2, true, 0)
-    RUN(512, 1024, 2, 2, false, 0)
-    RUN(512, 1024, 2, 2, true, 1)
     RUN(512, 1024, 2, 2, true, 2)
-    RUN(512, 1024, 2, 4, true, 0)
+    RUN(512, 1024, 2, 2, true, 5)
     RUN(256, 1024, 4, 2, true, 0)
-    RUN(512, 2048, 2, 2, true, 0)
-    RUN(512, 2048, 4, 2, true, 0)
-    RUN(1024, 4096, 1, 2, true, 0)
-    RUN(1024, 4096, 1, 4, true, 0)
-    RUN(1024, 2048, 2, 2, true, 0)
-    RUN(512, 512, 2, 2, true, 0)
-    RUN(512, 512, 4, 2, true, 0)
-    RUN(1024, 1024, 2, 2, true, 0)
-    RUN(512, 1024, 1, 4, true, 0)
-    RUN(256, 1024, 2, 2, true, 0)
-    RUN(256, 512, 2, 2, true, 0)
+    RUN(256, 1024, 4, 2, true, 5)
     RUN(256, 256, 2, 2, true, 0)
+    RUN(256, 256, 2, 2, true, 5)
+    RUN(256, 512, 4, 2, true, 5)
+    RUN(512, 2048, 2, 2, true, 5)
   }
   return 0;
 }

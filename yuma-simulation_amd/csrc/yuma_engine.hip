@@ -1717,8 +1717,20 @@ struct BondArgs {
   float* Binst_out;
   float* dpart;
   int N, V, M, tiles, rowblocks, t0, t1;
-  int wsh;  // every scenario reads input slice t (yuma_run_shared)
+  int wsh;      // every scenario reads input slice t (yuma_run_shared)
+  int cblocks;  // k_bonds_elem: column blocks of CB miners per row block
 };
+
+// Layouts of the per-(slice, 64-miner tile, validator) dividend partials:
+// DP_TV [slice][tile][V] (k_bonds; k_bonds_elem on 64-miner tiles), DP_VT
+// [slice][V][tile] (k_bonds_elem on wide column blocks: a wave's four
+// 64-miner tiles of one row land in 16 contiguous bytes). k_finalize / k_dsum
+// add the tiles in the same order either way.
+enum DpLayout { DP_TV = 0, DP_VT = 1 };
+__device__ __forceinline__ long long dp_index(int layout, long long slice, int tile, int v, int tiles,
+                                              int V) {
+  return layout == DP_VT ? (slice * V + v) * (long long)tiles + tile : (slice * tiles + tile) * (long long)V + v;
+}
 
 template <int VARIANT, int NT, int R, bool VEC>
 __global__ __launch_bounds__(NT) void k_bonds(BondArgs A) {
@@ -1991,16 +2003,25 @@ __global__ __launch_bounds__(NT) void k_bonds(BondArgs A) {
 // (a register ring refilled as each epoch is consumed), so the per-epoch HBM
 // latency is hidden behind P-1 epochs of work.
 // ---------------------------------------------------------------------------
-template <int VARIANT, int R, bool VEC, int P, bool VECI, bool NT = false>
-__global__ __launch_bounds__(256) void k_bonds_elem(BondArgs A) {
-  constexpr int G = 16;
-  const Lay L = lay();
-  const int tile = blockIdx.x % A.tiles;
-  const int rb = (blockIdx.x / A.tiles) % A.rowblocks;
-  const int n = blockIdx.x / (A.tiles * A.rowblocks);
+// Block shape: BS threads over CB miners x (G = BS / (CB/4)) rows per pass,
+// R passes, i.e. a block owns G R rows x CB miners of the bond state; lane
+// quads run along a row (CB/4 lanes per row), so a wave instruction moves
+// 4 rows x 256 B (CB = 64) or 1 row x 1 KiB (CB >= 256). The dividend partial
+// of each 64-miner tile is the 16-lane DPP sum of one DPP row in every shape.
+template <int VARIANT, int R, bool VEC, int P, bool VECI, bool NT = false, int BS = 256, int CB = 64,
+          int DPL = DP_TV>
+__global__ __launch_bounds__(BS) void k_bonds_elem(BondArgs A) {
+  constexpr int LPR = CB / 4, G = BS / LPR;
+  static_assert(CB % 64 == 0 && BS % LPR == 0, "a 16-lane DPP row must cover one 64-miner tile");
+  const int cq = threadIdx.x % LPR, lane = threadIdx.x & 63;
+  const int cb = blockIdx.x % A.cblocks;
+  const int rb = (blockIdx.x / A.cblocks) % A.rowblocks;
+  const int n = blockIdx.x / (A.cblocks * A.rowblocks);
   const int N = A.N, V = A.V, M = A.M;
   const long long VM = (long long)V * M;
-  const int m = tile * kTileM + L.c4 * 4;
+  const int m = cb * CB + cq * 4;
+  const int tile = m >> 6;  // this lane's 64-miner tile (dividend partials)
+  const int g = threadIdx.x / LPR;
   // every parameter is read once into registers: a global load inside the
   // epoch loop would make the compiler drain the prefetch ring (vmcnt(0))
   const yuma_params_t& pg = A.prm[n];
@@ -2009,7 +2030,7 @@ __global__ __launch_bounds__(256) void k_bonds_elem(BondArgs A) {
   const bool reset_all = (pg.flags & YUMA_FLAG_RESET_ALL_COLUMNS) != 0;
   const float p_bond_alpha = pg.bond_alpha, p_omba = pg.one_minus_bond_alpha;
   const float p_maxint = pg.maxint, p_capacity_alpha = pg.capacity_alpha, p_decay_keep = pg.decay_keep;
-  const int row0 = rb * G * R + L.g;
+  const int row0 = rb * G * R + g;
 
   float B[R][4];
   bool has_old;
@@ -2144,7 +2165,8 @@ __global__ __launch_bounds__(256) void k_bonds_elem(BondArgs A) {
             if (m + c < M) d = d + B[i][c] * ri[k][c];
         }
         d = wsum16(d);  // sum_row16's xor-butterfly tree, on DPP
-        if (L.c4 == 0 && row < V) A.dpart[(slice * A.tiles + tile) * V + row] = d;
+        if ((lane & 15) == 0 && row < V && tile < A.tiles)
+          A.dpart[dp_index(DPL, slice, tile, row, A.tiles, V)] = d;
       }
       has_old = true;
       if (t + P < A.t1) fetch(k, t + P);
@@ -2168,7 +2190,7 @@ __global__ __launch_bounds__(256) void k_finalize(const float* __restrict__ dpar
                                                   const float* __restrict__ tvc,
                                                   const float* __restrict__ tvn,
                                                   float* __restrict__ Dn, float* __restrict__ D,
-                                                  float* __restrict__ Tv) {
+                                                  float* __restrict__ Tv, int dpl) {
   // thread (tg, vq): tile group tg = tid / 64 sums tiles tg, tg+4, ...; vq owns
   // validators 4vq..4vq+3 of the current 256-validator window. Fixed order:
   // per-group sequential, then groups 0..3.
@@ -2178,7 +2200,36 @@ __global__ __launch_bounds__(256) void k_finalize(const float* __restrict__ dpar
   const long long slice = slice0 + blockIdx.x;
   const int tg = threadIdx.x >> 6, vq = threadIdx.x & 63;
   const float* dp = dpart + slice * (long long)tiles * V;
-  for (int v0 = 0; v0 < V; v0 += 256) {
+  if (dpl == DP_VT) {
+    // [V][tile]: one thread per validator walks its contiguous tiles, keeping
+    // the four tile-group sums of the [tile][V] path apart (tile k goes to
+    // group k % 4), then adds the groups in order: the same bits
+    for (int v = threadIdx.x; v < V; v += 256) {
+      const float* pv = dp + (long long)v * tiles;
+      float pg[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+      int k = 0;
+      if ((tiles & 3) == 0) {
+#pragma unroll 4
+        for (; k < tiles; k += 4) {
+          const float4 x = *reinterpret_cast<const float4*>(pv + k);
+          pg[0] = pg[0] + x.x;
+          pg[1] = pg[1] + x.y;
+          pg[2] = pg[2] + x.z;
+          pg[3] = pg[3] + x.w;
+        }
+      } else {
+        for (; k < tiles; ++k) pg[k & 3] = pg[k & 3] + pv[k];
+      }
+      float d = pg[0];
+      d = d + pg[1];
+      d = d + pg[2];
+      d = d + pg[3];
+      if (variant == YUMA_VARIANT_YUMA4) d = sn[slice * V + v] * d;
+      dsh[v] = d;
+    }
+    __syncthreads();
+  }
+  for (int v0 = 0; v0 < V && dpl == DP_TV; v0 += 256) {
     float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
     const int vb = v0 + vq * 4;
     if ((V & 3) == 0 && vb < V) {
@@ -2278,11 +2329,11 @@ __global__ __launch_bounds__(64) void k_rsum(const float* __restrict__ rpart, in
 }
 // per slice and validator: sum over this shard's tiles of the dividend partials
 __global__ __launch_bounds__(256) void k_dsum(const float* __restrict__ dpart, int V, int tiles,
-                                              float* __restrict__ out) {
+                                              float* __restrict__ out, int dpl) {
   const long long slice = blockIdx.x;
   for (int v = threadIdx.x; v < V; v += 256) {
     float d = 0.0f;
-    for (int k = 0; k < tiles; ++k) d = d + dpart[(slice * tiles + k) * V + v];
+    for (int k = 0; k < tiles; ++k) d = d + dpart[dp_index(dpl, slice, k, v, tiles, V)];
     out[slice * V + v] = d;
   }
 }
@@ -2519,8 +2570,13 @@ void launch_rank(RowCfg rc, long long nblocks, hipStream_t st, const float* W, c
   }
 }
 
+// Column-normalised variants (Rust / Yuma1 / Yuma2): one block owns whole
+// 64-miner columns (single row block). Returns the dividend-partial layout.
 template <int VARIANT, bool VEC>
-void launch_bonds_colnorm(RowCfg rc, long long nblocks, hipStream_t st, const yk::BondArgs& A) {
+int launch_bonds_colnorm(RowCfg rc, hipStream_t st, yk::BondArgs& A) {
+  A.rowblocks = 1;
+  A.cblocks = A.tiles;
+  const long long nblocks = (long long)A.N * A.tiles;
   switch (rc) {
     case RC_256_1:
       YK_LAUNCH((yk::k_bonds<VARIANT, 256, 1, VEC>), nblocks, 256, st, A);
@@ -2535,49 +2591,62 @@ void launch_bonds_colnorm(RowCfg rc, long long nblocks, hipStream_t st, const yk
       YK_LAUNCH((yk::k_bonds<VARIANT, 1024, 16, VEC>), nblocks, 1024, st, A);
       break;
   }
+  return yk::DP_TV;
 }
 
-// Element-wise variants (Yuma3 / Yuma4): 256 threads, R rows x 4 miners per
-// thread (16 R-row blocks), the inputs of the next P epochs in flight, float4
-// incentive / bond_alpha loads. Measured on MI355X at c2 (tools/ab_bonds.sh,
-// DESIGN.md section 2): writing the bond history, R = 2, P = 2 with
-// non-temporal history stores (Yuma3 1.68 ms, Yuma4 liquid 1.72 ms, against
-// 1.81 / 2.66 for R = 1, P = 4 and per-column loads); without the history,
-// R = 1, P = 4 (1.13 ms vs 1.36 for R = 2).
-// Rows per thread of k_bonds_elem: 2 where the scan has the VALU to spare
-// per column load (the history stream; shared-input sweeps, whose W reads hit
-// the caches, 11.4 -> 10.4 ms at c3), 1 for a bare HBM-bound scan (c2
-// without history: 1.13 vs 1.36 ms).
+// Element-wise variants (Yuma3 / Yuma4): R rows x 4 miners per thread, the
+// inputs of the next P epochs in flight, float4 incentive / bond_alpha loads.
+// Measured on MI355X at c2 (tools/ab_bonds.sh): without
+// the history, R = 1, P = 4 on 64-miner tiles (1.13 ms vs 1.36 for R = 2);
+// shared-input sweeps (W reads served by the caches) R = 2, P = 2.
+// Writing the bond history (the c2 line): wide column blocks, one row per
+// wave instruction (tools/scanbw: a 4-row x 4 KiB block footprint streams
+// the 4 GB in + 4 GB out at 5.6-5.9 TB/s against 5.0 for 32 rows x 256 B).
+#ifndef YK_WIDE_SCAN
+#define YK_WIDE_SCAN 1
+#endif
 int bonds_rows(bool vec, bool hist, bool wsh) { return vec && (hist || wsh) ? 2 : 1; }
+template <int VARIANT, int R, bool VEC, int P, bool VECI, bool NT, int BS, int CB, int DPL>
+int launch_elem_shape(hipStream_t st, yk::BondArgs& A) {
+  constexpr int G = BS / (CB / 4);
+  A.rowblocks = (A.V + G * R - 1) / (G * R);
+  A.cblocks = (A.M + CB - 1) / CB;
+  const long long nblocks = (long long)A.N * A.rowblocks * A.cblocks;
+  YK_LAUNCH((yk::k_bonds_elem<VARIANT, R, VEC, P, VECI, NT, BS, CB, DPL>), nblocks, BS, st, A);
+  return DPL;
+}
 template <int VARIANT, bool VEC>
-void launch_bonds_elem(long long nblocks, hipStream_t st, const yk::BondArgs& A) {
-  if (bonds_rows(VEC, A.B_hist != nullptr, A.wsh) != 2)
-    YK_LAUNCH((yk::k_bonds_elem<VARIANT, 1, VEC, 4, VEC, false>), nblocks, 256, st, A);
-  else if (A.B_hist != nullptr)
-    YK_LAUNCH((yk::k_bonds_elem<VARIANT, 2, VEC, 2, VEC, true>), nblocks, 256, st, A);
-  else
-    YK_LAUNCH((yk::k_bonds_elem<VARIANT, 2, VEC, 2, VEC, false>), nblocks, 256, st, A);
+int launch_bonds_elem(hipStream_t st, yk::BondArgs& A) {
+  const bool hist = A.B_hist != nullptr;
+  if constexpr (VEC) {
+    if (hist && YK_WIDE_SCAN == 1 && A.M >= 1024)
+      return launch_elem_shape<VARIANT, 2, true, 2, true, true, 512, 1024, yk::DP_VT>(st, A);
+    if (hist && YK_WIDE_SCAN == 2 && A.M >= 256)
+      return launch_elem_shape<VARIANT, 2, true, 2, true, true, 256, 256, yk::DP_VT>(st, A);
+    if (hist && YK_WIDE_SCAN == 3 && A.M >= 1024)
+      return launch_elem_shape<VARIANT, 4, true, 2, true, true, 256, 1024, yk::DP_VT>(st, A);
+  }
+  if (bonds_rows(VEC, hist, A.wsh != 0) != 2)
+    return launch_elem_shape<VARIANT, 1, VEC, 4, VEC, false, 256, 64, yk::DP_TV>(st, A);
+  if (hist) return launch_elem_shape<VARIANT, 2, VEC, 2, VEC, true, 256, 64, yk::DP_TV>(st, A);
+  return launch_elem_shape<VARIANT, 2, VEC, 2, VEC, false, 256, 64, yk::DP_TV>(st, A);
 }
 
+// Launch the bond scan for A.N scenarios over epochs [A.t0, A.t1); returns
+// the layout of the dividend partials it wrote (k_finalize / k_dsum read it).
 template <bool VEC>
-void launch_bonds(int variant, RowCfg rc, long long nblocks, hipStream_t st,
-                  const yk::BondArgs& A) {
+int launch_bonds(int variant, RowCfg rc, hipStream_t st, yk::BondArgs& A) {
   switch (variant) {
     case YUMA_VARIANT_RUST:
-      launch_bonds_colnorm<YUMA_VARIANT_RUST, VEC>(rc, nblocks, st, A);
-      break;
+      return launch_bonds_colnorm<YUMA_VARIANT_RUST, VEC>(rc, st, A);
     case YUMA_VARIANT_YUMA1:
-      launch_bonds_colnorm<YUMA_VARIANT_YUMA1, VEC>(rc, nblocks, st, A);
-      break;
+      return launch_bonds_colnorm<YUMA_VARIANT_YUMA1, VEC>(rc, st, A);
     case YUMA_VARIANT_YUMA2:
-      launch_bonds_colnorm<YUMA_VARIANT_YUMA2, VEC>(rc, nblocks, st, A);
-      break;
+      return launch_bonds_colnorm<YUMA_VARIANT_YUMA2, VEC>(rc, st, A);
     case YUMA_VARIANT_YUMA3:
-      launch_bonds_elem<YUMA_VARIANT_YUMA3, VEC>(nblocks, st, A);
-      break;
+      return launch_bonds_elem<YUMA_VARIANT_YUMA3, VEC>(st, A);
     default:
-      launch_bonds_elem<YUMA_VARIANT_YUMA4, VEC>(nblocks, st, A);
-      break;
+      return launch_bonds_elem<YUMA_VARIANT_YUMA4, VEC>(st, A);
   }
 }
 
@@ -2644,9 +2713,6 @@ int run_impl(int variant, const yuma_params_t* prm, int N, int E, int V, int M, 
   // one chunk by default: phase 1 of every epoch, then one bond scan
   if (chunk <= 0 || chunk > E) chunk = E;
 
-  const int colnorm = variant <= YUMA_VARIANT_YUMA2;
-  const int brows = 16 * bonds_rows(vec, out->B_hist != nullptr, wsh != 0);  // rows per bond block
-  const int rowblocks = colnorm ? 1 : (V + brows - 1) / brows;
 
   // Shared inputs: scenarios with the same consensus parameters take one
   // representative's consensus, quantisation input and (streaming) rank
@@ -2734,19 +2800,14 @@ int run_impl(int variant, const yuma_params_t* prm, int N, int E, int V, int M, 
     A.V = V;
     A.M = M;
     A.tiles = tiles;
-    A.rowblocks = rowblocks;
     A.t0 = c0;
     A.t1 = c1;
     A.wsh = wsh;
-    const long long nb = (long long)N * tiles * rowblocks;
     tm.mark(YUMA_PHASE_BONDS);
-    if (vec)
-      launch_bonds<true>(variant, rc, nb, st, A);
-    else
-      launch_bonds<false>(variant, rc, nb, st, A);
+    const int dpl = vec ? launch_bonds<true>(variant, rc, st, A) : launch_bonds<false>(variant, rc, st, A);
     tm.mark(YUMA_PHASE_FINALIZE);
     YK_LAUNCH(yk::k_finalize, ns, 256, st, ws.dpart, ws.sn, variant, V, s0, tiles, ws.tvc,
-              ws.tvn, out->Dn, out->D, out->Tv);
+              ws.tvn, out->Dn, out->D, out->Tv, dpl);
     if (out->Sn != nullptr)
       (void)hipMemcpyAsync(out->Sn + s0 * V, ws.sn + s0 * V, (size_t)ns * V * 4,
                            hipMemcpyDeviceToDevice, st);
@@ -2859,8 +2920,8 @@ int shard_stage_impl(int stage, int variant, const yuma_params_t* prm, int N, in
                            out->Wn, out->Wc, ws.tvc, ws.tvn, 0);
       YK_LAUNCH(yk::k_rsum, ns, 64, st, ws.rpart, tiles, io->rsum_part);
       if (full) {
-        YK_LAUNCH(yk::k_dsum, ns, 256, st, ws.tvc, V, tiles, io->tv_part);
-        YK_LAUNCH(yk::k_dsum, ns, 256, st, ws.tvn, V, tiles, io->tv_part + ns * V);
+        YK_LAUNCH(yk::k_dsum, ns, 256, st, ws.tvc, V, tiles, io->tv_part, (int)yk::DP_TV);
+        YK_LAUNCH(yk::k_dsum, ns, 256, st, ws.tvn, V, tiles, io->tv_part + ns * V, (int)yk::DP_TV);
       }
       break;
     }
@@ -2894,16 +2955,10 @@ int shard_stage_impl(int stage, int variant, const yuma_params_t* prm, int N, in
       A.V = V;
       A.M = M;
       A.tiles = tiles;
-      const int brows = 16 * bonds_rows(vec, out->B_hist != nullptr, false);
-      A.rowblocks = variant <= YUMA_VARIANT_YUMA2 ? 1 : (V + brows - 1) / brows;
       A.t0 = 0;
       A.t1 = E;
-      const long long nb = (long long)N * tiles * A.rowblocks;
-      if (vec)
-        launch_bonds<true>(variant, rc, nb, st, A);
-      else
-        launch_bonds<false>(variant, rc, nb, st, A);
-      YK_LAUNCH(yk::k_dsum, ns, 256, st, ws.dpart, V, tiles, io->dsum_part);
+      const int dpl = vec ? launch_bonds<true>(variant, rc, st, A) : launch_bonds<false>(variant, rc, st, A);
+      YK_LAUNCH(yk::k_dsum, ns, 256, st, ws.dpart, V, tiles, io->dsum_part, dpl);
       break;
     }
     case 5: {
@@ -2911,7 +2966,7 @@ int shard_stage_impl(int stage, int variant, const yuma_params_t* prm, int N, in
       if (full && !io->tv) return fail(YUMA_EINVAL, "stage 5 with out->Tv needs io->tv");
       YK_LAUNCH(yk::k_finalize, ns, 256, st, io->dsum, ws.sn, variant, V, 0LL, 1,
                 full ? io->tv : nullptr, full ? io->tv + ns * V : nullptr, out->Dn, out->D,
-                out->Tv);
+                out->Tv, (int)yk::DP_TV);
       if (out->Sn != nullptr)
         (void)hipMemcpyAsync(out->Sn, ws.sn, (size_t)ns * V * 4, hipMemcpyDeviceToDevice, st);
       if (out->alpha_ab != nullptr)
