@@ -2601,7 +2601,12 @@ int launch_bonds_colnorm(RowCfg rc, hipStream_t st, yk::BondArgs& A) {
 // shared-input sweeps (W reads served by the caches) R = 2, P = 2.
 // Writing the bond history (the c2 line): wide column blocks, one row per
 // wave instruction (tools/scanbw: a 4-row x 4 KiB block footprint streams
-// the 4 GB in + 4 GB out at 5.6-5.9 TB/s against 5.0 for 32 rows x 256 B).
+// the 4 GB in + 4 GB out at 5.6-5.9 TB/s against 5.0 for 32 rows x 256 B;
+// in the engine c2 Yuma 3 bonds 1.66-1.72 -> 1.54-1.58 ms). Without the
+// history the same shapes lose (c2 1.05 -> 1.07-1.69 ms, c4 1.63 -> 1.63-1.84,
+// the c3 sweep 10.2 -> 10.6-14.7 ms: profiles/r03/ab/scan_shapes_nohist.txt).
+// (YK_WIDE_SCAN=0 builds the 64-miner-tile scan everywhere: the A/B
+// harness, tools/ab_scan.sh)
 #ifndef YK_WIDE_SCAN
 #define YK_WIDE_SCAN 1
 #endif
@@ -2619,12 +2624,8 @@ template <int VARIANT, bool VEC>
 int launch_bonds_elem(hipStream_t st, yk::BondArgs& A) {
   const bool hist = A.B_hist != nullptr;
   if constexpr (VEC) {
-    if (hist && YK_WIDE_SCAN == 1 && A.M >= 1024)
+    if (hist && YK_WIDE_SCAN && A.M >= 1024)
       return launch_elem_shape<VARIANT, 2, true, 2, true, true, 512, 1024, yk::DP_VT>(st, A);
-    if (hist && YK_WIDE_SCAN == 2 && A.M >= 256)
-      return launch_elem_shape<VARIANT, 2, true, 2, true, true, 256, 256, yk::DP_VT>(st, A);
-    if (hist && YK_WIDE_SCAN == 3 && A.M >= 1024)
-      return launch_elem_shape<VARIANT, 4, true, 2, true, true, 256, 1024, yk::DP_VT>(st, A);
   }
   if (bonds_rows(VEC, hist, A.wsh != 0) != 2)
     return launch_elem_shape<VARIANT, 1, VEC, 4, VEC, false, 256, 64, yk::DP_TV>(st, A);
