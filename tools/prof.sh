@@ -9,7 +9,7 @@ export TMPDIR=/tmp
 TAG=$1; shift
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
-B=(python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-also --profile-reps 1 "$@")
+B=(python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-also --profile-reps 1 "$@")
 run() {
   local name=$1; shift
   echo "== $TAG $name"
