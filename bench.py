@@ -86,12 +86,15 @@ PHASE_KERNELS = {"rowsum": "k_rowsum", "consensus": "k_consensus_w", "quantise":
                  "rank": "k_rank_s", "incentive": "k_incentive", "finalize": "k_finalize"}
 
 
-def kernel_of(phase: str, variant: int) -> str:
+def kernel_of(phase: str, variant: int, shared: bool = False) -> str:
     """The kernel that runs a phase (as rocprofv3 names it) for run outputs:
-    the bond scan is k_bonds_elem for Yuma 3/4 and k_bonds (column-normalised
-    EMA) for YumaRust / Yuma 1 / Yuma 2."""
+    the bond scan is k_bonds_elem for Yuma 3/4 (k_bonds_grp for a sweep over
+    one shared input trajectory) and k_bonds (column-normalised EMA) for
+    YumaRust / Yuma 1 / Yuma 2."""
     if phase == "bonds":
-        return "k_bonds_elem" if variant >= 3 else "k_bonds"
+        if variant >= 3:
+            return "k_bonds_grp" if shared else "k_bonds_elem"
+        return "k_bonds"
     return PHASE_KERNELS[phase]
 
 
@@ -334,11 +337,11 @@ def engine_line(args, variant: int, params: list, W, S, world: int, dist: bool, 
         if phases[i] <= 0:
             continue
         b = phase_bytes(name, V, M, variant, liquid, hist, eff_chunk, wshare) * units
-        phase_info[name] = {"kernel": kernel_of(name, variant), "ms": round(float(phases[i]), 4),
+        phase_info[name] = {"kernel": kernel_of(name, variant, shared), "ms": round(float(phases[i]), 4),
                             "GBps": round(b / (phases[i] * 1e-3) / 1e9, 1)}
     dom = int(np.argmax(phases))
     dom_name = engine.PHASES[dom]
-    dom_kernel = kernel_of(dom_name, variant)
+    dom_kernel = kernel_of(dom_name, variant, shared)
     dom_bytes = phase_bytes(dom_name, V, M, variant, liquid, hist, eff_chunk, wshare) * units / launches
     dom_ms = float(phases[dom]) / launches
     k_achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
@@ -388,9 +391,10 @@ def engine_line(args, variant: int, params: list, W, S, world: int, dist: bool, 
             "unit": "GB/s",
             "frac": None if achieved is None else round(achieved / HBM_PEAK_GBPS, 4),
             "traffic": traffic,
-            "definition": ("measured HBM bytes of one step (rocprofv3 FETCH_SIZE + WRITE_SIZE, "
-                           f"{os.path.relpath(TRAFFIC_JSON, ROOT)}) / the step time / 8 TB/s; the kernel record counts "
-                           "W once per input epoch for all scenarios (each input read once)"),
+            "definition": ("measured bytes beyond L2 of one step (rocprofv3 FETCH_SIZE + WRITE_SIZE, "
+                           f"{os.path.relpath(TRAFFIC_JSON, ROOT)}; Infinity-Cache hits count as fetched) / the step "
+                           "time / 8 TB/s; the kernel record counts W once per input epoch for all scenarios (each "
+                           "input read once)"),
             "equivalent_GBps": round(equivalent, 1),
             "equivalent_definition": (f"scenario-epochs/s per GPU x the per-scenario epoch-step contract "
                                       f"{contract:,.0f} B: a rate, not traffic (every scenario reads one shared "
@@ -504,6 +508,27 @@ def bench_wide(args, world: int, rank: int, dist: bool) -> dict:
                         "traffic": None if pmc is None else round(sum(pmc.values()) * E),
                         "definition": "SURVEY 8d step roofline per GPU: BYTES(V, M/world) x epochs/s / 8 TB/s "
                                       "(all stages and exchanges inside the wall time)"}
+    if not dist:
+        # per-phase device time of the same run (HIP events, yuma_run_profiled)
+        # and the dominant kernel's roofline, as for c2
+        buf = [0.0] * len(engine.PHASES)
+        engine.run(variant, params, W, S, want_hist=hist, workspace=ws, phase_ms=buf)
+        liquid = any(p.liquid_mode != engine.LIQUID_OFF for p in params)
+        phases = {}
+        for i, name in enumerate(engine.PHASES):
+            if buf[i] > 0:
+                b = phase_bytes(name, V, M, variant, liquid, hist, E) * E
+                phases[name] = {"kernel": kernel_of(name, variant), "ms": round(buf[i], 4),
+                                "GBps": round(b / (buf[i] * 1e-3) / 1e9, 1)}
+        dom = max(phases, key=lambda k: phases[k]["ms"])
+        dk = kernel_of(dom, variant)
+        db = phase_bytes(dom, V, M, variant, liquid, hist, E) * E
+        line["roofline"]["kernel"] = {
+            "name": dk, "launches_per_step": 1, "avg_ms": phases[dom]["ms"], "bytes_per_launch": db,
+            "achieved": phases[dom]["GBps"], "frac": round(phases[dom]["GBps"] / HBM_PEAK_GBPS, 4),
+            "traffic": None if pmc is None or dk not in pmc else round(pmc[dk] * E),
+            "timing": "HIP events on the launch stream around the kernel (yuma_run_profiled)"}
+        line["phases"] = phases
     if rank == 0 and not args.no_cpu_baseline and variant in (3, 4):
         Wc = engine.synth_weights(args.seed, 3, 1, V, M)  # the full-width first epochs, for the CPU
         line["cpu_baseline"] = cpu_baseline({3: "yuma3", 4: "yuma4"}[variant], Wc, S, [YumaConfig()], 10.0, 1, 0,

@@ -283,10 +283,18 @@ def test_bench_line_helpers():
         for phase in engine.PHASES:
             assert bench.kernel_of(phase, variant).startswith("k_")
     assert bench.kernel_of("bonds", engine.VARIANT_YUMA3) == "k_bonds_elem"
+    assert bench.kernel_of("bonds", engine.VARIANT_YUMA4, shared=True) == "k_bonds_grp"
     key = {"V": 256, "M": 4096, "epochs": 1000, "scenarios_per_gpu": 1, "version": "Yuma 3 (Rhef)",
            "bond_history": True}
     pmc = bench.load_traffic(key)
     assert pmc is not None and pmc["k_bonds_elem"] > 8e6
+    # every bench config has a committed traffic record (c3: the grouped scan)
+    c3 = bench.load_traffic({"V": 256, "M": 4096, "epochs": 32, "scenarios_per_gpu": 512,
+                             "version": "Yuma 4 (Rhef+relative bonds)", "bond_history": False})
+    assert c3 is not None and "k_bonds_grp" in c3
+    c4 = bench.load_traffic({"V": 256, "M": 65536, "epochs": 100, "scenarios_per_gpu": 1,
+                             "version": "Yuma 3 (Rhef)", "bond_history": False})
+    assert c4 is not None and "k_consensus_w" in c4
     assert bench.load_traffic(dict(key, M=1)) is None
     assert bench.contract_bytes(256, 4096, 3) == 12_617_728
 

@@ -2165,6 +2165,9 @@ __global__ __launch_bounds__(BS) void k_bonds_elem(BondArgs A) {
             if (m + c < M) d = d + B[i][c] * ri[k][c];
         }
         d = wsum16(d);  // sum_row16's xor-butterfly tree, on DPP
+#ifdef YK_DIAG_NO_DP  // timing-only build: the partials' stores left out (wrong dividends)
+        if (d == 1.2345e-37f)
+#endif
         if ((lane & 15) == 0 && row < V && tile < A.tiles)
           A.dpart[dp_index(DPL, slice, tile, row, A.tiles, V)] = d;
       }
@@ -2176,6 +2179,195 @@ __global__ __launch_bounds__(BS) void k_bonds_elem(BondArgs A) {
   for (int i = 0; i < R; ++i) {
     const int row = row0 + G * i;
     if (row < V) store4<VEC>(A.Bstate + n * VM + (long long)row * M, m, M, B[i]);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Phase 2 for parameter sweeps over ONE input trajectory (shared inputs,
+// config c3), element-wise variants: a block runs the scan of K scenarios
+// side by side over one 16 R-row x 64-miner tile of W. Every scenario of the
+// sweep reads the same W[t]; k_bonds_elem's per-scenario blocks fetch W once
+// per scenario from beyond L2 (69.6 GB per c3 step: profiles/r03/c3). Here
+// W[t], the row sums and the normalised weights are loaded and divided once
+// per K scenarios; each scenario keeps its own bond tile in registers and its
+// own parameters, resets, liquid bond_alpha and dividend partials — the same
+// operations in the same order as k_bonds_elem, so the same bits. The scan
+// is VALU-bound, not fetch-bound: c3 bonds 10.4 ms (K = 1) -> 9.9 (K = 2),
+// 10.3 (K = 4), 15.1 (K = 8: 204 VGPRs and SGPR spills), same box
+// (profiles/r03/ab/c3_scan_groups.txt); the saving is the shared division.
+// ---------------------------------------------------------------------------
+template <int VARIANT, int K, int R, int P>
+__global__ __launch_bounds__(256) void k_bonds_grp(BondArgs A) {
+  constexpr int G = 16;
+  const Lay L = lay();
+  const int tile = blockIdx.x % A.tiles;
+  const int rb = (blockIdx.x / A.tiles) % A.rowblocks;
+  const int n0 = (blockIdx.x / (A.tiles * A.rowblocks)) * K;
+  const int N = A.N, V = A.V, M = A.M;
+  const long long VM = (long long)V * M;
+  const int m = tile * kTileM + L.c4 * 4;
+  const int row0 = rb * G * R + L.g;
+  const int nk = N - n0 < K ? N - n0 : K;  // scenarios of this block (block-uniform)
+
+  // every parameter read once into registers (a load inside the epoch loop
+  // would wait on the prefetches, see k_bonds_elem)
+  float p_ba[K], p_omba[K], p_maxint[K], p_ca[K], p_dk[K];
+  int p_rmode[K], p_repoch[K], p_rindex[K];
+  unsigned liquid_mask = 0, rall_mask = 0;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const yuma_params_t& pg = A.prm[min(n0 + k, N - 1)];
+    p_ba[k] = pg.bond_alpha;
+    p_omba[k] = pg.one_minus_bond_alpha;
+    p_maxint[k] = pg.maxint;
+    p_ca[k] = pg.capacity_alpha;
+    p_dk[k] = pg.decay_keep;
+    p_rmode[k] = pg.reset_mode;
+    p_repoch[k] = pg.reset_epoch;
+    p_rindex[k] = pg.reset_index;
+    if (pg.liquid_mode != YUMA_LIQUID_OFF) liquid_mask |= 1u << k;
+    if (pg.flags & YUMA_FLAG_RESET_ALL_COLUMNS) rall_mask |= 1u << k;
+  }
+
+  float B[K][R][4];
+  bool has_old;
+  {
+    const float* src = A.t0 == 0 ? A.B_init : A.Bstate;
+    has_old = src != nullptr;
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        const int row = row0 + G * i;
+        if (has_old && k < nk && row < V)
+          load4<true>(src + (n0 + k) * VM + (long long)row * M, m, M, B[k][i]);
+        else
+#pragma unroll
+          for (int c = 0; c < 4; ++c) B[k][i][c] = 0.0f;
+      }
+  }
+
+  // the shared inputs of the next P epochs in flight: W rows and the row
+  // sums / stakes (k_rowsum stored them for every scenario; scenario n0's)
+  float rw[P][R][4], rd[P][R], rsn[P][R];
+  auto fetch = [&](int kk, int t) {
+    const long long slice = (long long)t * N + n0;
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const int rr = min(row0 + G * i, V - 1);
+      load4c<true>(A.W + (long long)t * VM, rr, V, m, M, rw[kk][i]);
+      rd[kk][i] = A.rsd[slice * V + rr];
+      rsn[kk][i] = A.sn[slice * V + rr];
+    }
+  };
+  // per scenario: incentive and liquid bond_alpha of the epoch in use, each
+  // refilled with the next epoch's as soon as it is consumed
+  float ri[K][4], rba[K][4];
+  auto fetch_s = [&](int k, int t) {
+    const long long slice = (long long)t * N + min(n0 + k, N - 1);
+    load4c<true>(A.I + slice * M, 0, 1, m, M, ri[k]);
+    if (liquid_mask & (1u << k)) load4c<true>(A.ba + slice * M, 0, 1, m, M, rba[k]);
+  };
+#pragma unroll
+  for (int kk = 0; kk < P; ++kk)
+    if (A.t0 + kk < A.t1) fetch(kk, A.t0 + kk);
+#pragma unroll
+  for (int k = 0; k < K; ++k) fetch_s(k, A.t0);
+
+  for (int tb = A.t0; tb < A.t1; tb += P) {
+#pragma unroll
+    for (int kk = 0; kk < P; ++kk) {
+      const int t = tb + kk;
+      if (t >= A.t1) break;
+      // normalised weights, once for the K scenarios
+      float wn[R][4];
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        const RowDiv rdv = row_div(rd[kk][i]);
+        bool slow = false;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) wn[i][c] = div_fast_nz(rw[kk][i][c], rdv, slow);
+        if (__any(slow)) {
+#pragma unroll
+          for (int c = 0; c < 4; ++c) wn[i][c] = rw[kk][i][c] / rd[kk][i];
+        }
+      }
+      float sv[R];
+#pragma unroll
+      for (int i = 0; i < R; ++i) sv[i] = rsn[kk][i];
+      if (t + P < A.t1) fetch(kk, t + P);
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        if (k >= nk) break;
+        const long long slice = (long long)t * N + n0 + k;
+        const bool liquid = (liquid_mask >> k) & 1u;
+        const bool reset_all = (rall_mask >> k) & 1u;
+        const int reset_mode = p_rmode[k], reset_index = p_rindex[k];
+        if (has_old && reset_mode != YUMA_RESET_NONE && t == p_repoch[k] &&
+            (reset_all || (reset_index >= 0 && reset_index < M))) {
+          bool fire = reset_mode == YUMA_RESET_ALWAYS;
+          if (reset_mode == YUMA_RESET_IF_ZERO_CONSENSUS && t >= 1 && !reset_all)
+            fire = A.C[(slice - N) * M + reset_index] == 0.0f;
+          const int c = reset_index - m;
+          if (fire && (reset_all || (c >= 0 && c < 4)))
+#pragma unroll
+            for (int i = 0; i < R; ++i)
+#pragma unroll
+              for (int cc = 0; cc < 4; ++cc)
+                if (reset_all || cc == c) B[k][i][cc] = 0.0f;
+        }
+        float bac[4], omba[4], ic[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          bac[c] = liquid ? rba[k][c] : p_ba[k];
+          omba[c] = liquid ? 1.0f - rba[k][c] : p_omba[k];
+          ic[c] = ri[k][c];
+        }
+        if (t + 1 < A.t1) fetch_s(k, t + 1);
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+          const int row = row0 + G * i;
+          // k_bonds_elem's short clamp forms (signed zeros cannot show, see there)
+          if (VARIANT == YUMA_VARIANT_YUMA3) {
+            const float cap = sv[i] * p_maxint[k];
+            const float ca = p_ca[k] * cap;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+              const float rem = vmax(cap - B[k][i][c], 0.0f);
+              const float pc = vmin(ca, rem);
+              const float nb = p_dk[k] * B[k][i][c] + pc * wn[i][c];
+              B[k][i][c] = tmin(nb, cap);
+            }
+          } else {
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+              const float bd = B[k][i][c] * omba[c];
+              const float rem = vmax(1.0f - bd, 0.0f);
+              const float nb = bd + vmin(bac[c] * wn[i][c], rem);
+              B[k][i][c] = vmin(nb, 1.0f);
+            }
+          }
+          if (A.B_hist != nullptr && row < V)
+            store4<true>(A.B_hist + slice * VM + (long long)row * M, m, M, B[k][i]);
+          float d = 0.0f;
+          if (m < M)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) d = d + B[k][i][c] * ic[c];
+          d = wsum16(d);
+          if (L.c4 == 0 && row < V) A.dpart[(slice * A.tiles + tile) * V + row] = d;
+        }
+      }
+      has_old = true;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    if (k >= nk) break;
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const int row = row0 + G * i;
+      if (row < V) store4<true>(A.Bstate + (n0 + k) * VM + (long long)row * M, m, M, B[k][i]);
+    }
   }
 }
 
@@ -2610,6 +2802,11 @@ int launch_bonds_colnorm(RowCfg rc, hipStream_t st, yk::BondArgs& A) {
 #ifndef YK_WIDE_SCAN
 #define YK_WIDE_SCAN 1
 #endif
+// scenarios per block of the shared-input scan (k_bonds_grp); 1 = one
+// scenario per block (k_bonds_elem), the A/B baseline
+#ifndef YK_SCAN_GROUP
+#define YK_SCAN_GROUP 2
+#endif
 int bonds_rows(bool vec, bool hist, bool wsh) { return vec && (hist || wsh) ? 2 : 1; }
 template <int VARIANT, int R, bool VEC, int P, bool VECI, bool NT, int BS, int CB, int DPL>
 int launch_elem_shape(hipStream_t st, yk::BondArgs& A) {
@@ -2626,6 +2823,16 @@ int launch_bonds_elem(hipStream_t st, yk::BondArgs& A) {
   if constexpr (VEC) {
     if (hist && YK_WIDE_SCAN && A.M >= 1024)
       return launch_elem_shape<VARIANT, 2, true, 2, true, true, 512, 1024, yk::DP_VT>(st, A);
+  }
+  if constexpr (VEC) {
+    if (A.wsh && A.N >= 2 && YK_SCAN_GROUP > 1) {  // a sweep over one input trajectory
+      constexpr int K = YK_SCAN_GROUP, R = 1;
+      A.rowblocks = (A.V + 16 * R - 1) / (16 * R);
+      A.cblocks = A.tiles;
+      const long long nblocks = (long long)((A.N + K - 1) / K) * A.rowblocks * A.tiles;
+      YK_LAUNCH((yk::k_bonds_grp<VARIANT, K, R, 2>), nblocks, 256, st, A);
+      return yk::DP_TV;
+    }
   }
   if (bonds_rows(VEC, hist, A.wsh != 0) != 2)
     return launch_elem_shape<VARIANT, 1, VEC, 4, VEC, false, 256, 64, yk::DP_TV>(st, A);
