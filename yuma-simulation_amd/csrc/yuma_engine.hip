@@ -843,7 +843,7 @@ __device__ __forceinline__ void prerank_store(const float (&wn)[R][4], const flo
 // Consensus (see k_consensus for the search argument), wave-owned columns.
 // HIST: exact-stake histogram finish (below); kHB grid points per column,
 // kHS words per column in LDS (16-B aligned, 4-bank skew between columns).
-constexpr int kHB = 64, kHS = 68;
+constexpr int kHB = 64, kHS = 68, kHistMinW = 8;
 constexpr int kHistWords = 4 * 16 * kHS;  // one block: 4 waves x 16 columns
 
 // The consensus search of this lane's 4 columns over the wave's normalised
@@ -983,31 +983,45 @@ __device__ __forceinline__ void consensus_search(const float (&wn)[R][4], const 
     thr = ut - (kd > 33554432.0 ? 33554432 : (int)kd);
   }
   for (;;) {
-    bool active = false;
+    for (;;) {
+      bool active = false;
 #pragma unroll
-    for (int c = 0; c < 4; ++c) active |= (hi_k[c] - lo_k[c]) > lim;
-    if (!__any(active)) break;
-    float part[4], midf[4];
-    int mid[4];
+      for (int c = 0; c < 4; ++c) active |= (hi_k[c] - lo_k[c]) > lim;
+      if (!__any(active)) break;
+      float part[4], midf[4];
+      int mid[4];
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      mid[c] = (lo_k[c] + hi_k[c]) >> 1;
-      midf[c] = (float)mid[c] * inv_scale;
-      part[c] = 0.0f;
+      for (int c = 0; c < 4; ++c) {
+        mid[c] = (lo_k[c] + hi_k[c]) >> 1;
+        midf[c] = (float)mid[c] * inv_scale;
+        part[c] = 0.0f;
+      }
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        const float zs = 0.0f * s[i];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) part[c] = part[c] + ((wn[i][c] > midf[c]) ? s[i] : zs);
+      }
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        part[c] = red_sum<LPC>(part[c]);
+        const bool act = hi_k[c] - lo_k[c] > lim, up = part[c] > kappa;
+        lo_k[c] = (act && up) ? mid[c] : lo_k[c];
+        hi_k[c] = (act && !up) ? mid[c] : hi_k[c];
+      }
     }
+    // Brackets of at most kHistMinW grid points (a wide subnet's tiny
+    // normalised weights: c4) put every row of a column into a few bins, and
+    // the histogram's LDS atomics to one address serialise; such waves finish
+    // with <= 3 more bisection passes instead (the same result: the
+    // histogram finish equals the bisection, test_consensus_hist.py)
+    if (!hist) break;
+    bool wide = false;
 #pragma unroll
-    for (int i = 0; i < R; ++i) {
-      const float zs = 0.0f * s[i];
-#pragma unroll
-      for (int c = 0; c < 4; ++c) part[c] = part[c] + ((wn[i][c] > midf[c]) ? s[i] : zs);
-    }
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      part[c] = red_sum<LPC>(part[c]);
-      const bool act = hi_k[c] - lo_k[c] > lim, up = part[c] > kappa;
-      lo_k[c] = (act && up) ? mid[c] : lo_k[c];
-      hi_k[c] = (act && !up) ? mid[c] : hi_k[c];
-    }
+    for (int c = 0; c < 4; ++c) wide |= (hi_k[c] - lo_k[c]) > kHistMinW;
+    if (__any(wide)) break;
+    hist = false;
+    lim = 1;
   }
   {
     if (hist) {
@@ -1327,6 +1341,20 @@ __device__ double block_sum_d(double x, double* red) {
   return t;
 }
 
+// high-byte histogram of the levels (four loads in flight per thread)
+template <int NT>
+__device__ void hist_high(const int* __restrict__ q, int M, int* hist1) {
+  int j = threadIdx.x;
+  for (; j + 3 * NT < M; j += 4 * NT) {
+    int v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = min(max(q[j + u * NT], 0), 65535);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) atomicAdd(&hist1[v[u] >> 8], 1);
+  }
+  for (; j < M; j += NT) atomicAdd(&hist1[min(max(q[j], 0), 65535) >> 8], 1);
+}
+
 // k-th smallest quantisation level (0-based) by a two-level 256-bin integer
 // histogram select. Integer counts are order independent, so the selection is
 // exact and deterministic. hist1 must already hold the high-byte histogram.
@@ -1345,7 +1373,18 @@ __device__ int select_level(const int* __restrict__ q, int M, int k, const int* 
   for (int j = threadIdx.x; j < 256; j += NT) hist2[j] = 0;
   __syncthreads();
   const int b = bc[0];
-  for (int j = threadIdx.x; j < M; j += NT) {
+  // four levels in flight per thread (a wide subnet has 65536 per slice and
+  // one block per slice: the loop is L2-latency-bound otherwise)
+  int j = threadIdx.x;
+  for (; j + 3 * NT < M; j += 4 * NT) {
+    int v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = min(max(q[j + u * NT], 0), 65535);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if ((v[u] >> 8) == b) atomicAdd(&hist2[v[u] & 255], 1);
+  }
+  for (; j < M; j += NT) {
     const int v = min(max(q[j], 0), 65535);
     if ((v >> 8) == b) atomicAdd(&hist2[v & 255], 1);
   }
@@ -1419,12 +1458,28 @@ __global__ __launch_bounds__(NT) void k_quantise(const double* __restrict__ craw
     }
   } else if (variant == YUMA_VARIANT_RUST) {
     double acc = 0.0;
-    for (int m = threadIdx.x; m < M; m += NT) acc = acc + cr[m];
+    int m = threadIdx.x;
+    for (; m + 3 * NT < M; m += 4 * NT) {  // loads in flight, same summation order
+      const double x0 = cr[m], x1 = cr[m + NT], x2 = cr[m + 2 * NT], x3 = cr[m + 3 * NT];
+      acc = acc + x0;
+      acc = acc + x1;
+      acc = acc + x2;
+      acc = acc + x3;
+    }
+    for (; m < M; m += NT) acc = acc + cr[m];
     sumd = block_sum_d<NT>(acc, redd);
     sumf = (float)sumd;
   } else {
     float acc = 0.0f;
-    for (int m = threadIdx.x; m < M; m += NT) acc = acc + (float)cr[m];
+    int m = threadIdx.x;
+    for (; m + 3 * NT < M; m += 4 * NT) {  // loads in flight, same summation order
+      const double x0 = cr[m], x1 = cr[m + NT], x2 = cr[m + 2 * NT], x3 = cr[m + 3 * NT];
+      acc = acc + (float)x0;
+      acc = acc + (float)x1;
+      acc = acc + (float)x2;
+      acc = acc + (float)x3;
+    }
+    for (; m < M; m += NT) acc = acc + (float)cr[m];
     sumf = block_sum<NT>(acc, redf);
   }
   for (int m = threadIdx.x; m < M; m += NT) {
@@ -1450,7 +1505,7 @@ __global__ __launch_bounds__(NT) void k_quantise(const double* __restrict__ craw
     } else {
       for (int j = threadIdx.x; j < 256; j += NT) hist1[j] = 0;
       __syncthreads();
-      for (int m = threadIdx.x; m < M; m += NT) atomicAdd(&hist1[min(max(q[m], 0), 65535) >> 8], 1);
+      hist_high<NT>(q, M, hist1);
       __syncthreads();
       const bool H = p.override_flags & YUMA_OVR_HIGH, Lw = p.override_flags & YUMA_OVR_LOW;
       ch = H ? (float)p.override_high : quantile_of<NT>(q, M, 0.75f, hist1, hist2, bc);
@@ -1606,7 +1661,7 @@ __global__ __launch_bounds__(NT) void k_liquid(const yuma_params_t* __restrict__
     } else if (qlev != nullptr) {  // (a shard caller that omits the levels gets NaN alphas)
       for (int j = threadIdx.x; j < 256; j += NT) hist1[j] = 0;
       __syncthreads();
-      for (int mm = threadIdx.x; mm < Mq; mm += NT) atomicAdd(&hist1[min(max(q[mm], 0), 65535) >> 8], 1);
+      hist_high<NT>(q, Mq, hist1);
       __syncthreads();
       const bool H = p.override_flags & YUMA_OVR_HIGH, Lw = p.override_flags & YUMA_OVR_LOW;
       ch = H ? (float)p.override_high : quantile_of<NT>(q, Mq, 0.75f, hist1, hist2, bc);
