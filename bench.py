@@ -216,9 +216,19 @@ def cpu_baseline(variant: str, W_dev, S_dev, cfgs: list, seconds: float, warmup:
     }
 
 
+PREWARM_S = 1.0
+
+
 def timed(step, warmup: int, steps: int, dist: bool, dev) -> float:
-    """W untimed warmups, then K steps between barrier + synchronize; the
-    max over ranks of the elapsed wall time."""
+    """An untimed clock ramp (steps repeated for PREWARM_S seconds: an idle
+    MI355X takes ~6 c2 steps to reach its steady clocks, profiles/r03/c2y3
+    kernel_trace.csv), W untimed warmups, then K steps between barrier +
+    synchronize; the max over ranks of the elapsed wall time."""
+    t_end = time.perf_counter() + PREWARM_S
+    while time.perf_counter() < t_end:
+        for _ in range(8):
+            step()
+        torch.cuda.synchronize()
     for _ in range(warmup):
         step()
     torch.cuda.synchronize()
