@@ -283,3 +283,27 @@ def test_torch_cpu_run_simulation_matches_sheet(sheet, bi):
             got = np.array([div[v] for v in case.validators]).T
             tag = f"b{beta} {case.name[:7]} {version}"
             np.testing.assert_array_equal(got, g["dividends"][bi, ci, vi], err_msg=tag)
+
+
+@pytest.mark.parametrize("bi", [0, 3])
+def test_dividends_per_1000_tao_bitwise(sheet, bi):
+    """The host-side dividend formatting of run_simulations
+    (simulation_utils._dividends_per_1000_tao: the reference's tensor ops,
+    then the Python-double ratio, simulation_utils.py:48-49,95-107) turns the
+    reference's own normalised dividends into the reference's dividend lists
+    bit for bit (CPU only: the golden Dn stand in for the engine's)."""
+    import torch
+
+    from yuma_simulation._internal.simulation_utils import _dividends_per_1000_tao
+
+    g, _ = sheet
+    beta = specs.BETAS[bi]
+    for ci, case in enumerate(cases):
+        W, S = case.packed_inputs()
+        for vi in range(len(specs.VERSIONS)):
+            cfg = sheet_config(beta, vi)
+            Dn = torch.from_numpy(np.ascontiguousarray(g["dn"][bi, ci, vi]))
+            div = _dividends_per_1000_tao(case, cfg, S, Dn)
+            got = np.array([div[v] for v in case.validators]).T
+            np.testing.assert_array_equal(got, g["dividends"][bi, ci, vi], err_msg=f"{case.name} {vi}")
+            assert all(type(x) is float for v in case.validators for x in div[v])

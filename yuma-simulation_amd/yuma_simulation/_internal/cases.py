@@ -100,6 +100,19 @@ class BaseCase:
         """[E, V] float32 stakes."""
         return torch.stack(self.stakes_epochs)
 
+    def packed_inputs(self) -> tuple[torch.Tensor, torch.Tensor]:
+        """([E, V, M] weights, [E, V] stakes) of the first num_epochs epochs,
+        built once per case and shared: read-only (run_simulations stacks them
+        into the engine's batch; the public *_epochs properties keep handing
+        out fresh copies as the reference does)."""
+        def make():
+            E = self.num_epochs
+            W = torch.stack(list(self.weights_epochs)[:E]).to(torch.float32)
+            S = torch.stack(list(self.stakes_epochs)[:E]).to(torch.float32)
+            return W, S
+
+        return self._cached("_packed", make)
+
 
 def create_case(case_name: str, **kwargs) -> BaseCase:
     if case_name not in class_registry:

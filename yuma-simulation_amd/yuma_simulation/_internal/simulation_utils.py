@@ -18,6 +18,7 @@ from __future__ import annotations
 from collections import defaultdict
 from dataclasses import dataclass
 
+import numpy as np
 import pandas as pd
 import torch
 
@@ -68,16 +69,14 @@ def _dividends_per_1000_tao(case: BaseCase, config: YumaConfig, S: torch.Tensor,
     reciprocal multiply), then the Python-double ratio. This is O(E*V) output
     formatting, not the hot path."""
     stakes_tao = S * config.total_subnet_stake
-    stakes_units = (stakes_tao / 1000.0).tolist()
+    stakes_units = (stakes_tao / 1000.0).numpy().astype(np.float64)  # float(x.item()): exact widening
     E_i = config.validator_emission_ratio * Dn
-    emission = (E_i * config.total_epoch_emission).tolist()
-    out: dict[str, list[float]] = {v: [] for v in case.validators}
-    for e in range(len(stakes_units)):
-        for i, validator in enumerate(case.validators):
-            stake_unit = float(stakes_units[e][i])
-            emission_i = float(emission[e][i])
-            out[validator].append(emission_i / stake_unit if stake_unit > 1e-6 else 0.0)
-    return out
+    emission = (E_i * config.total_epoch_emission).numpy().astype(np.float64)
+    # the Python-double ratio, elementwise in IEEE double (the same bits)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        ratio = np.where(stakes_units > 1e-6, emission / stakes_units, 0.0)
+    cols = ratio.T.tolist()
+    return {validator: cols[i] for i, validator in enumerate(case.validators)}
 
 
 def run_simulations(runs: list[SimulationRun], *, want_bonds: bool = True,
@@ -89,8 +88,7 @@ def run_simulations(runs: list[SimulationRun], *, want_bonds: bool = True,
     packed = []
     for k, r in enumerate(runs):
         variant, reset_mode = resolve_version(r.yuma_version)
-        W = torch.stack(list(r.case.weights_epochs)[: r.case.num_epochs]).to(torch.float32)
-        S = torch.stack(list(r.case.stakes_epochs)[: r.case.num_epochs]).to(torch.float32)
+        W, S = r.case.packed_inputs()
         packed.append((variant, reset_mode, W, S))
         groups[(variant,) + tuple(W.shape)].append(k)
 

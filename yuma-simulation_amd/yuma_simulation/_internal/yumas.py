@@ -11,7 +11,7 @@ of the input ``W`` (CPU in, CPU out — as the reference returns them).
 
 from __future__ import annotations
 
-from dataclasses import asdict, dataclass, field
+from dataclasses import dataclass, field, fields
 
 import torch
 
@@ -53,9 +53,11 @@ class YumaConfig:
     yuma_params: YumaParams = field(default_factory=YumaParams)
 
     def __post_init__(self):
+        # the reference copies asdict(group) onto the instance; every field is
+        # an immutable scalar or None, so copying the attributes is the same
         for group in (self.simulation, self.yuma_params):
-            for key, value in asdict(group).items():
-                setattr(self, key, value)
+            for f in fields(group):
+                setattr(self, f.name, getattr(group, f.name))
 
 
 @dataclass(frozen=True)
