@@ -217,6 +217,9 @@ def cpu_baseline(variant: str, W_dev, S_dev, cfgs: list, seconds: float, warmup:
 
 
 PREWARM_S = 1.0
+# torch.distributed backend of the N-rank run: "nccl" (RCCL over xGMI, one GPU
+# per rank); "gloo" only to rehearse the multi-rank path on a one-GPU box
+BACKEND = os.environ.get("YUMA_BENCH_BACKEND", "nccl")
 
 
 def timed(step, warmup: int, steps: int, dist: bool, dev) -> float:
@@ -225,10 +228,22 @@ def timed(step, warmup: int, steps: int, dist: bool, dev) -> float:
     kernel_trace.csv), W untimed warmups, then K steps between barrier +
     synchronize; the max over ranks of the elapsed wall time."""
     t_end = time.perf_counter() + PREWARM_S
-    while time.perf_counter() < t_end:
+    while True:
         for _ in range(8):
             step()
         torch.cuda.synchronize()
+        done = time.perf_counter() >= t_end
+        if dist:
+            # every rank must run the same number of steps: a step may hold
+            # collectives (c4's shard exchanges), so the ranks agree on when
+            # the ramp ends
+            import torch.distributed as tdist
+
+            f = torch.tensor([1.0 if done else 0.0], device="cpu" if BACKEND == "gloo" else dev)
+            tdist.all_reduce(f, op=tdist.ReduceOp.MAX)
+            done = bool(f.item() > 0)
+        if done:
+            break
     for _ in range(warmup):
         step()
     torch.cuda.synchronize()
@@ -245,7 +260,7 @@ def timed(step, warmup: int, steps: int, dist: bool, dev) -> float:
         tdist.barrier()
     elapsed = time.perf_counter() - t0
     if dist:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        t = torch.tensor([elapsed], device="cpu" if BACKEND == "gloo" else dev, dtype=torch.float64)
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
         elapsed = float(t.item())
     return elapsed
@@ -702,13 +717,21 @@ def main():
     if dist:
         import torch.distributed as tdist
 
-        torch.cuda.set_device(local)
-        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if BACKEND == "gloo":
+            # rehearsal of the N-rank path on a box with fewer GPUs: ranks share
+            # the card(s), collectives go through host memory
+            torch.cuda.set_device(local % torch.cuda.device_count())
+            tdist.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(local)
+            tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
     run = {"c2": bench_engine, "c3": bench_engine, "c4": bench_wide, "c5": bench_sheet}[args.config]
     line = run(args, world, rank, dist)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist:
+        # rank 0 may still be timing its CPU baseline: leave together
+        tdist.barrier()
         tdist.destroy_process_group()
 
 

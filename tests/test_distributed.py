@@ -156,3 +156,50 @@ def test_engine_scenario_sharding_gloo_world2(n_total, shared):
         np.testing.assert_array_equal(C, full.C.cpu().numpy())
         np.testing.assert_array_equal(I, full.I.cpu().numpy())
         np.testing.assert_array_equal(Bf, full.B_final[local[0]:local[-1] + 1].cpu().numpy())
+
+
+def _timed_worker(rank, world, port, q):
+    """bench.timed with a collective inside the step (c4's shard exchanges)
+    and ranks of different speed: the clock ramp must end on the same step
+    on every rank, or the ranks' collectives pair up wrongly and hang."""
+    import sys
+    import time
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), YUMA_BENCH_BACKEND="gloo")
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), ".."))
+    import bench
+
+    torch.cuda.synchronize = lambda *a, **k: None  # CPU-only rehearsal
+    bench.PREWARM_S = 0.3
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        n = [0]
+
+        def step():
+            time.sleep(0.002 if rank == 0 else 0.02)  # rank 1 is 10x slower
+            t = torch.ones(1)
+            dist.all_reduce(t)
+            n[0] += 1
+
+        if rank == 1:
+            time.sleep(0.5)  # ranks reach the timing at different moments
+        elapsed = bench.timed(step, 2, 3, True, torch.device("cpu"))
+        q.put((rank, n[0], elapsed))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_timed_ranks_agree_on_step_count():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_timed_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = sorted(q.get(timeout=60) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert got[0][1] == got[1][1]  # same number of steps on both ranks
+    assert got[0][2] == got[1][2]  # the max over ranks, on every rank
