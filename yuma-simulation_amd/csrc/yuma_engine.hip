@@ -719,7 +719,7 @@ __device__ __forceinline__ float qsum4(float x) {
 }
 
 // Load + normalise this lane's R rows x 4 miners of a slice (branch-free).
-template <int R, bool VEC, bool SIGNED0 = true>
+template <int R, bool VEC>
 __device__ __forceinline__ void load_norm_w(const float* __restrict__ Ws, const float* rsd_s,
                                             const float* sn_s, int V, int M, int m, int rg,
                                             float (&wn)[R][4], float (&s)[R]) {
@@ -755,49 +755,11 @@ __device__ __forceinline__ void load_norm_w(const float* __restrict__ Ws, const 
     }
   }
   bool slow = false;
-  if constexpr (SIGNED0) {
 #pragma unroll
-    for (int i = 0; i < R; ++i) {
-      const RowDiv rdv = row_div(d[i]);
+  for (int i = 0; i < R; ++i) {
+    const RowDiv rdv = row_div(d[i]);
 #pragma unroll
-      for (int c = 0; c < 4; ++c) wn[i][c] = div_fast(wn[i][c], rdv, slow);
-    }
-  } else {
-    // div_fast_nz on packed pairs (v_pk_mul / v_pk_fma: two lanes' worth of
-    // fp32 per instruction), with the operand guard reduced to a lane-wide
-    // max |a| (NaN-ignoring: the fast path returns the same quiet NaN as
-    // IEEE division) and a min over nonzero |a| taken on 2·bits(|a|) - 1
-    // (zeros wrap to the maximum), instead of three compares per element.
-    typedef float f2 __attribute__((ext_vector_type(2)));
-    float amax = 0.0f, dmin = INFINITY;
-    unsigned ymin = 0xFFFFFFFFu;
-    // The four DPP rows of a wave hold the same 16·R validator rows, so each
-    // lane computes the IEEE reciprocal of R/4 of them (row 4j + cq) and
-    // the rest arrive by ds_bpermute from lane rg + 16·(i & 3).
-#pragma unroll
-    for (int i = 0; i < R; ++i) {
-      const float r = 1.0f / d[i];
-      amax = fmaxf(amax, fabsf(d[i]));
-      dmin = fminf(dmin, fabsf(d[i]));
-      const f2 r2 = {r, r}, nd2 = {-d[i], -d[i]};
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const f2 a2 = {wn[i][2 * h], wn[i][2 * h + 1]};
-#pragma unroll
-        for (int c = 0; c < 2; ++c) {
-          amax = fmaxf(amax, fabsf(a2[c]));
-          const unsigned y = (__float_as_uint(a2[c]) << 1) - 1u;
-          ymin = y < ymin ? y : ymin;
-        }
-        const f2 q = a2 * r2;
-        const f2 e = __builtin_elementwise_fma(nd2, q, a2);
-        const f2 q1 = __builtin_elementwise_fma(e, r2, q);
-        wn[i][2 * h] = q1[0];
-        wn[i][2 * h + 1] = q1[1];
-      }
-    }
-    slow = !(dmin >= 0x1p-60f && amax <= 0x1p60f &&
-             (ymin == 0xFFFFFFFFu || ymin + 1u >= (__float_as_uint(0x1p-60f) << 1)));
+    for (int c = 0; c < 4; ++c) wn[i][c] = div_fast(wn[i][c], rdv, slow);
   }
   if (__any(slow)) {  // rare: some operand outside the fast-division guard
 #pragma unroll
@@ -816,11 +778,135 @@ __device__ __forceinline__ void load_norm_w(const float* __restrict__ Ws, const 
   }
 }
 
+// The consensus kernel's load + normalise. The wave's row sums, stakes and row
+// reciprocals are staged in a wave-private LDS copy `rl` ([16 R] row sums,
+// [16 R] stakes with 0 on padding rows, [16 R] RN(1 / row sum)) instead of
+// 2 x R VGPRs per lane (166 -> 127 VGPRs, 4 waves / SIMD): the row-sum / stake
+// loads go out first, the W loads behind them, and the copy is written while
+// W is in flight. Each IEEE reciprocal is computed once per wave (by the lane
+// that stages the row) instead of once per column quad.
+// Division: div_fast_nz's sequence (q = a·r, e = fma(-d, q, a), q + e·r) on
+// packed pairs (v_pk_mul / v_pk_fma: two lanes' worth of fp32 per
+// instruction), with the operand guard reduced to a lane-wide max |a| (NaN-
+// ignoring: the fast path returns the same quiet NaN as IEEE division) and a
+// min over nonzero |a| taken on 2·bits(|a|) - 1 (zeros wrap to the maximum),
+// instead of three compares per element; no signed-zero fix-up (consensus
+// only compares normalised weights against grid points >= 0).
+template <int R, bool VEC>
+__device__ __forceinline__ void load_norm_w_lds(const float* __restrict__ Ws, const float* rsd_s,
+                                                const float* sn_s, float* rl, int V, int M, int m,
+                                                int rg, int lane, float (&wn)[R][4]) {
+  constexpr int NR = 16 * R, PL = (NR + 63) / 64;
+  float dv[PL], sv[PL];
+#pragma unroll
+  for (int k = 0; k < PL; ++k) {
+    const int jj = min(lane + 64 * k, V - 1);
+    dv[k] = rsd_s[jj];
+    sv[k] = sn_s[jj];
+  }
+  const bool full = rg + 16 * (R - 1) < V && m + 3 < M;
+  const bool allfull = VEC && __all(full) && (long long)V * M < (1ll << 30);
+#ifdef YK_DIAG_CONS_NOLOAD  // timing-only: weights made up from the indices, no W read
+  if (allfull) {
+#pragma unroll
+    for (int i = 0; i < R; ++i)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) wn[i][c] = (float)(((rg + 16 * i) * 37 + (m + c) * 11) & 4095);
+  } else
+#else
+  if (allfull) {
+    const unsigned o0 = (unsigned)rg * (unsigned)M + (unsigned)m, st = 16u * (unsigned)M;
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const float4 t = *reinterpret_cast<const float4*>(Ws + (o0 + (unsigned)i * st));
+      wn[i][0] = t.x;
+      wn[i][1] = t.y;
+      wn[i][2] = t.z;
+      wn[i][3] = t.w;
+    }
+  } else
+#endif
+  {
+#pragma unroll
+    for (int i = 0; i < R; ++i) load4c<VEC>(Ws, rg + 16 * i, V, m, M, wn[i]);
+  }
+  // the division guard's row-sum part over the staged rows (the guard is
+  // wave-wide: __any below)
+  float amax = 0.0f, dmin = INFINITY;
+#pragma unroll
+  for (int k = 0; k < PL; ++k) {
+    const int j = lane + 64 * k;
+    amax = fmaxf(amax, fabsf(dv[k]));
+    dmin = fminf(dmin, fabsf(dv[k]));
+    if (j < NR) {
+      rl[j] = dv[k];
+      rl[NR + j] = j < V ? sv[k] : 0.0f;
+      rl[2 * NR + j] = 1.0f / dv[k];
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  // packed division, row sums and reciprocals from LDS
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  unsigned ymin = 0xFFFFFFFFu;
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    const float d = rl[rg + 16 * i];
+    const float r = rl[2 * NR + rg + 16 * i];
+    const f2 r2 = {r, r}, nd2 = {-d, -d};
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const f2 a2 = {wn[i][2 * h], wn[i][2 * h + 1]};
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        amax = fmaxf(amax, fabsf(a2[c]));
+        const unsigned y = (__float_as_uint(a2[c]) << 1) - 1u;
+        ymin = y < ymin ? y : ymin;
+      }
+      const f2 q = a2 * r2;
+      const f2 e = __builtin_elementwise_fma(nd2, q, a2);
+      const f2 q1 = __builtin_elementwise_fma(e, r2, q);
+      wn[i][2 * h] = q1[0];
+      wn[i][2 * h + 1] = q1[1];
+    }
+  }
+  const bool slow = !(dmin >= 0x1p-60f && amax <= 0x1p60f &&
+                      (ymin == 0xFFFFFFFFu || ymin + 1u >= (__float_as_uint(0x1p-60f) << 1)));
+  if (__any(slow)) {  // rare: some operand outside the fast-division guard
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      load4c<VEC>(Ws, rg + 16 * i, V, m, M, wn[i]);
+      const float d = rl[rg + 16 * i];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) wn[i][c] = wn[i][c] / d;
+    }
+  }
+  if (!__all(full)) {
+#pragma unroll
+    for (int i = 0; i < R; ++i) mask4(rg + 16 * i, V, m, M, wn[i]);
+  }
+}
+
 // P = sum_v S·Wn (yumas.py:192) for this lane's 4 columns: product rounded,
 // then summed (no FMA), two columns per packed v_pk_mul / v_pk_add; row
 // order rg + 16 i per lane, then the 16-lane DPP tree.
-template <int R>
-__device__ __forceinline__ void prerank_store(const float (&wn)[R][4], const float (&s)[R],
+// Stakes of a lane's rows rg + 16 i read from a wave-private LDS copy on
+// every use instead of 16 VGPRs (k_consensus_w). `off` goes through an empty
+// asm at each pass (`fresh`), so the compiler cannot hoist the reads out of
+// the search loops back into registers.
+struct LdsRows {
+  const float* base;  // a __shared__ array
+  int off;
+  __device__ __forceinline__ float operator[](int i) const { return base[off + 16 * i]; }
+};
+__device__ __forceinline__ LdsRows fresh(LdsRows s) {
+  asm volatile("" : "+v"(s.off));
+  return s;
+}
+
+template <int R, typename SV>
+__device__ __forceinline__ void prerank_store(const float (&wn)[R][4], const SV& s,
                                               const WLay& L, int m, int M, float* __restrict__ Pout) {
   typedef float f2 __attribute__((ext_vector_type(2)));
   f2 a01 = {0.0f, 0.0f}, a23 = {0.0f, 0.0f};
@@ -893,8 +979,8 @@ __device__ __forceinline__ int red_iscan_excl(int x, int rg) {
 
 // LPC lanes per column quad: lane (cq, rg) holds rows rg + LPC i of columns
 // 4 cq .. 4 cq + 3 of the wave's 256 / LPC columns.
-template <int R, int LPC>
-__device__ __forceinline__ void consensus_search(const float (&wn)[R][4], const float (&s)[R],
+template <int R, int LPC, typename SV>
+__device__ __forceinline__ void consensus_search(const float (&wn)[R][4], const SV& s,
                                                  float kappa, int iters, int ut, unsigned* hb,
                                                  int lane, int cq, int rg, int (&hi_k)[4]) {
   constexpr int NCOL = 256 / LPC;  // columns per wave
@@ -996,11 +1082,13 @@ __device__ __forceinline__ void consensus_search(const float (&wn)[R][4], const 
         midf[c] = (float)mid[c] * inv_scale;
         part[c] = 0.0f;
       }
+      const auto& sp = fresh(s);
 #pragma unroll
       for (int i = 0; i < R; ++i) {
-        const float zs = 0.0f * s[i];
+        const float si = sp[i];
+        const float zs = 0.0f * si;
 #pragma unroll
-        for (int c = 0; c < 4; ++c) part[c] = part[c] + ((wn[i][c] > midf[c]) ? s[i] : zs);
+        for (int c = 0; c < 4; ++c) part[c] = part[c] + ((wn[i][c] > midf[c]) ? si : zs);
       }
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
@@ -1031,24 +1119,28 @@ __device__ __forceinline__ void consensus_search(const float (&wn)[R][4], const 
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      unsigned su[R];  // stakes in units of 2^-24 (exact, checked above)
-#pragma unroll
-      for (int i = 0; i < R; ++i) su[i] = (unsigned)(s[i] * 16777216.0f);
+      float nlo[4];
+      unsigned w[4];
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
-        unsigned* cb = wb + (cq * 4 + c) * kHS;
-        const float nlo = -(float)lo_k[c];
-        const unsigned w = (unsigned)(hi_k[c] - lo_k[c]);
+        nlo[c] = -(float)lo_k[c];
+        w[c] = (unsigned)(hi_k[c] - lo_k[c]);
+      }
+      const auto& sp = fresh(s);
+      // rows outer: one stake conversion per row (integer atomics: any order)
 #pragma unroll
-        for (int i = 0; i < R; ++i) {
+      for (int i = 0; i < R; ++i) {
+        const unsigned su = (unsigned)(sp[i] * 16777216.0f);  // stake in 2^-24 units (exact, checked above)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
           // bin = clamp(ceil(wn·2^iters) - lo, 0, w). wn·2^iters is exact,
           // and so is its difference with the integer lo whenever it is
           // >= 0 (both are multiples of ulp(wn·2^iters)); anything that
           // rounds is negative and lands in bin 0 either way. The u32
           // convert saturates (negatives and -inf -> 0, +inf -> max) and
           // maps NaN to 0, i.e. never above a grid point, as `>` does.
-          const unsigned k = (unsigned)ceilf(fmaf(wn[i][c], scale, nlo));
-          atomicAdd(cb + (k < w ? k : w), su[i]);
+          const unsigned k = (unsigned)ceilf(fmaf(wn[i][c], scale, nlo[c]));
+          atomicAdd(wb + (cq * 4 + c) * kHS + (k < w[c] ? k : w[c]), su);
         }
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1083,7 +1175,7 @@ __device__ __forceinline__ void consensus_search(const float (&wn)[R][4], const 
 }
 
 template <int R, bool VEC>
-__global__ __launch_bounds__(256, 3) void k_consensus_w(const float* __restrict__ W,
+__global__ __launch_bounds__(256, 4) void k_consensus_w(const float* __restrict__ W,
                                                      const float* __restrict__ rsd,
                                                      const float* __restrict__ sn,
                                                      const int* __restrict__ sx,
@@ -1100,9 +1192,22 @@ __global__ __launch_bounds__(256, 3) void k_consensus_w(const float* __restrict_
   if (dup_slice(crep, slice, N)) return;  // block-uniform
   const int m = tile * kTileM + L.wave * 16 + L.cq * 4;
   if (tile * kTileM + L.wave * 16 >= M) return;  // whole wave past the last miner
-  float wn[R][4], s[R];
-  load_norm_w<R, VEC, false>(W + in_slice(slice, N, wsh) * (long long)V * M, rsd + slice * V,
-                             sn + slice * V, V, M, m, L.rg, wn, s);
+  __shared__ __attribute__((aligned(16))) float rl[4][48 * R];
+  float wn[R][4];
+  load_norm_w_lds<R, VEC>(W + in_slice(slice, N, wsh) * (long long)V * M, rsd + slice * V,
+                          sn + slice * V, rl[L.wave], V, M, m, L.rg, L.lane, wn);
+  const LdsRows s{&rl[0][0], L.wave * 48 * R + 16 * R + L.rg};
+#ifdef YK_DIAG_CONS_LOADONLY  // timing-only: the W loads and division, nothing else
+  {
+    float t = 0.0f;
+#pragma unroll
+    for (int i = 0; i < R; ++i)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) t = t + wn[i][c];
+    if (t == 1234.5f) craw[slice * M + m] = t;
+    return;
+  }
+#endif
   if (Pout != nullptr) prerank_store<R>(wn, s, L, m, M, Pout + slice * M);
   int hi_k[4];
   const yuma_params_t& p = prm[n];
