@@ -13,14 +13,15 @@ typedef float fvec4 __attribute__((ext_vector_type(4)));
 
 // DP: per-epoch dividend partials like the scan's: one fp32 per (row, 64-column
 // sub-tile) from the 16 lanes of the sub-tile; 0 none, 1 stored [tile][V]
-// (the engine's dpart layout), 2 stored [V][tile]
+// (the engine's dpart layout), 2 stored [V][tile], 5 [column block][V][epoch]
+// [sub-tile], 6 [epoch][column block][V][sub-tile]
 template <int BS, int CB, int R, int P, bool NT, int DP = 0>
 __global__ __launch_bounds__(BS) void k_scan(const fvec4* __restrict__ x, fvec4* __restrict__ y, int steps,
                                              int V, int M, float* out) {
   constexpr int LPR = CB / 4, G = BS / LPR;
   const int tiles = M / CB;
   int tile = blockIdx.x % tiles, rb = blockIdx.x / tiles;
-  if (DP >= 3) {  // XCD-grouped: XCD x (= block % 8) owns a contiguous band of rows, every column block
+  if (DP == 3 || DP == 4) {  // XCD-grouped: XCD x (= block % 8) owns a contiguous band of rows, every column block
     const int x = blockIdx.x & 7, k = blockIdx.x >> 3, per = gridDim.x >> 3;
     const int band = per / tiles;  // row blocks per XCD
     tile = k / band;
@@ -59,6 +60,9 @@ __global__ __launch_bounds__(BS) void k_scan(const fvec4* __restrict__ x, fvec4*
             else if (DP == 5) {  // [column block][V][epoch][sub-tiles of the block]
               constexpr int TPB = CB / 64;
               out[1 + (((long long)tile * V + row) * steps + t) * TPB + (st % TPB)] = p;
+            } else if (DP == 6) {  // [epoch][column block][V][sub-tiles of the block]
+              constexpr int TPB = CB / 64;
+              out[1 + (((long long)t * tiles + tile) * V + row) * TPB + (st % TPB)] = p;
             } else out[1 + ((long long)t * V + row) * tl + st] = p;
           }
         }
@@ -112,18 +116,11 @@ int main() {
            P, NT ? "nt" : "", DP, blocks, G * R, CB * 4, ms, moved / ms / 1e6);                               \
     fflush(stdout);                                                                                           \
   }
-  for (int rep2 = 0; rep2 < 2; ++rep2) {
-    RUN(256, 64, 2, 2, true, 1)  // k_bonds_elem with history today
-    RUN(256, 64, 2, 2, true, 5)
-    RUN(512, 1024, 2, 2, true, 0)
-    RUN(512, 1024, 2, 2, true, 2)
+  for (int rep2 = 0; rep2 < 3; ++rep2) {
+    RUN(512, 1024, 2, 2, true, 0)  // no partials
+    RUN(512, 1024, 2, 2, true, 2)  // [epoch][V][sub-tile]: the engine's wide scan (round 3)
     RUN(512, 1024, 2, 2, true, 5)
-    RUN(256, 1024, 4, 2, true, 0)
-    RUN(256, 1024, 4, 2, true, 5)
-    RUN(256, 256, 2, 2, true, 0)
-    RUN(256, 256, 2, 2, true, 5)
-    RUN(256, 512, 4, 2, true, 5)
-    RUN(512, 2048, 2, 2, true, 5)
+    RUN(512, 1024, 2, 2, true, 6)
   }
   return 0;
 }
