@@ -2351,10 +2351,14 @@ __global__ __launch_bounds__(BS) void k_bonds_elem(BondArgs A) {
 // W[t], the row sums and the normalised weights are loaded and divided once
 // per K scenarios; each scenario keeps its own bond tile in registers and its
 // own parameters, resets, liquid bond_alpha and dividend partials — the same
-// operations in the same order as k_bonds_elem, so the same bits. The scan
-// is VALU-bound, not fetch-bound: c3 bonds 10.4 ms (K = 1) -> 9.9 (K = 2),
-// 10.3 (K = 4), 15.1 (K = 8: 204 VGPRs and SGPR spills), same box
-// (profiles/r03/ab/c3_scan_groups.txt); the saving is the shared division.
+// operations in the same order as k_bonds_elem, so the same bits. c3 bonds
+// 10.4 ms (K = 1) -> 9.9 (K = 2), 10.3 (K = 4), 15.1 (K = 8: 204 VGPRs and
+// SGPR spills), same box (profiles/r03/ab/c3_scan_groups.txt). The loop is
+// issue-bound, on the scalar side: per-lane pointers advanced by a stride
+// per epoch instead of 64-bit slice-index products took its SALU from 137 to
+// 38 per two epochs and its SGPR spills from 48 to 22 (9.9 -> 9.1 ms);
+// packed-pair f32 math (no gain: v_pk_* issue as two ops on gfx950) and an
+// XCD-grouped block order (9.4-9.5 ms) were tried and dropped.
 // ---------------------------------------------------------------------------
 template <int VARIANT, int K, int R, int P>
 __global__ __launch_bounds__(256) void k_bonds_grp(BondArgs A) {
@@ -2407,32 +2411,82 @@ __global__ __launch_bounds__(256) void k_bonds_grp(BondArgs A) {
       }
   }
 
+  // Addressing: per-lane pointers (load4c's clamped row and column folded
+  // in) that advance by a constant stride per epoch, instead of 64-bit
+  // slice-index products per epoch and scenario on the scalar unit: the loop
+  // was bound by scalar issue (137 SALU against 188 VALU per two epochs, and
+  // SGPR spills), not by the vector work (profiles/r03/c3sq).
+  const int mc = m < M ? m : M - 4;
+  const long long sV = (long long)N * V, sM = (long long)N * M, sD = (long long)N * A.tiles * V;
+
   // the shared inputs of the next P epochs in flight: W rows and the row
   // sums / stakes (k_rowsum stored them for every scenario; scenario n0's)
   float rw[P][R][4], rd[P][R], rsn[P][R];
-  auto fetch = [&](int kk, int t) {
-    const long long slice = (long long)t * N + n0;
+  const float* fW[R];  // next epoch to fetch
+  const float* fR[R];
+  const float* fS[R];
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    const int rr = min(row0 + G * i, V - 1);
+    fW[i] = A.W + (long long)A.t0 * VM + (long long)rr * M + mc;
+    fR[i] = A.rsd + ((long long)A.t0 * N + n0) * V + rr;
+    fS[i] = A.sn + ((long long)A.t0 * N + n0) * V + rr;
+  }
+  auto fetch = [&](int kk, bool load) {
 #pragma unroll
     for (int i = 0; i < R; ++i) {
-      const int rr = min(row0 + G * i, V - 1);
-      load4c<true>(A.W + (long long)t * VM, rr, V, m, M, rw[kk][i]);
-      rd[kk][i] = A.rsd[slice * V + rr];
-      rsn[kk][i] = A.sn[slice * V + rr];
+      if (load) {
+        const float4 x = *reinterpret_cast<const float4*>(fW[i]);
+        rw[kk][i][0] = x.x;
+        rw[kk][i][1] = x.y;
+        rw[kk][i][2] = x.z;
+        rw[kk][i][3] = x.w;
+        rd[kk][i] = *fR[i];
+        rsn[kk][i] = *fS[i];
+      }
+      fW[i] += VM;
+      fR[i] += sV;
+      fS[i] += sV;
     }
   };
   // per scenario: incentive and liquid bond_alpha of the epoch in use, each
   // refilled with the next epoch's as soon as it is consumed
   float ri[K][4], rba[K][4];
-  auto fetch_s = [&](int k, int t) {
-    const long long slice = (long long)t * N + min(n0 + k, N - 1);
-    load4c<true>(A.I + slice * M, 0, 1, m, M, ri[k]);
-    if (liquid_mask & (1u << k)) load4c<true>(A.ba + slice * M, 0, 1, m, M, rba[k]);
+  const float* fI[K];
+  const float* fB[K];
+  float* pD[K];  // this epoch's dividend partials (lane's first row)
+  float* pH[K];  // this epoch's bond history (lane's first row), if stored
+  const bool hist = A.B_hist != nullptr;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const long long s0 = (long long)A.t0 * N + min(n0 + k, N - 1);
+    fI[k] = A.I + s0 * M + mc;
+    fB[k] = A.ba + s0 * M + mc;
+    pD[k] = A.dpart + (s0 * A.tiles + tile) * V + row0;
+    pH[k] = hist ? A.B_hist + s0 * VM + (long long)row0 * M + m : nullptr;
+  }
+  auto fetch_s = [&](int k, bool load) {
+    if (load) {
+      const float4 x = *reinterpret_cast<const float4*>(fI[k]);
+      ri[k][0] = x.x;
+      ri[k][1] = x.y;
+      ri[k][2] = x.z;
+      ri[k][3] = x.w;
+      if (liquid_mask & (1u << k)) {
+        const float4 y = *reinterpret_cast<const float4*>(fB[k]);
+        rba[k][0] = y.x;
+        rba[k][1] = y.y;
+        rba[k][2] = y.z;
+        rba[k][3] = y.w;
+      }
+    }
+    fI[k] += sM;
+    fB[k] += sM;
   };
 #pragma unroll
-  for (int kk = 0; kk < P; ++kk)
-    if (A.t0 + kk < A.t1) fetch(kk, A.t0 + kk);
+  for (int kk = 0; kk < P; ++kk) fetch(kk, A.t0 + kk < A.t1);
 #pragma unroll
-  for (int k = 0; k < K; ++k) fetch_s(k, A.t0);
+  for (int k = 0; k < K; ++k) fetch_s(k, true);
 
   for (int tb = A.t0; tb < A.t1; tb += P) {
 #pragma unroll
@@ -2455,16 +2509,16 @@ __global__ __launch_bounds__(256) void k_bonds_grp(BondArgs A) {
       float sv[R];
 #pragma unroll
       for (int i = 0; i < R; ++i) sv[i] = rsn[kk][i];
-      if (t + P < A.t1) fetch(kk, t + P);
+      fetch(kk, t + P < A.t1);
 #pragma unroll
       for (int k = 0; k < K; ++k) {
         if (k >= nk) break;
-        const long long slice = (long long)t * N + n0 + k;
         const bool liquid = (liquid_mask >> k) & 1u;
         const bool reset_all = (rall_mask >> k) & 1u;
         const int reset_mode = p_rmode[k], reset_index = p_rindex[k];
-        if (has_old && reset_mode != YUMA_RESET_NONE && t == p_repoch[k] &&
-            (reset_all || (reset_index >= 0 && reset_index < M))) {
+        if (__builtin_expect(t == p_repoch[k] && has_old && reset_mode != YUMA_RESET_NONE &&
+                                 (reset_all || (reset_index >= 0 && reset_index < M)), 0)) {
+          const long long slice = (long long)t * N + n0 + k;
           bool fire = reset_mode == YUMA_RESET_ALWAYS;
           if (reset_mode == YUMA_RESET_IF_ZERO_CONSENSUS && t >= 1 && !reset_all)
             fire = A.C[(slice - N) * M + reset_index] == 0.0f;
@@ -2483,7 +2537,7 @@ __global__ __launch_bounds__(256) void k_bonds_grp(BondArgs A) {
           omba[c] = liquid ? 1.0f - rba[k][c] : p_omba[k];
           ic[c] = ri[k][c];
         }
-        if (t + 1 < A.t1) fetch_s(k, t + 1);
+        fetch_s(k, t + 1 < A.t1);
 #pragma unroll
         for (int i = 0; i < R; ++i) {
           const int row = row0 + G * i;
@@ -2507,15 +2561,18 @@ __global__ __launch_bounds__(256) void k_bonds_grp(BondArgs A) {
               B[k][i][c] = vmin(nb, 1.0f);
             }
           }
-          if (A.B_hist != nullptr && row < V)
-            store4<true>(A.B_hist + slice * VM + (long long)row * M, m, M, B[k][i]);
+          if (hist && row < V && m < M)
+            *reinterpret_cast<float4*>(pH[k] + (long long)G * i * M) =
+                make_float4(B[k][i][0], B[k][i][1], B[k][i][2], B[k][i][3]);
           float d = 0.0f;
           if (m < M)
 #pragma unroll
             for (int c = 0; c < 4; ++c) d = d + B[k][i][c] * ic[c];
           d = wsum16(d);
-          if (L.c4 == 0 && row < V) A.dpart[(slice * A.tiles + tile) * V + row] = d;
+          if (L.c4 == 0 && row < V) pD[k][G * i] = d;
         }
+        pD[k] += sD;
+        if (hist) pH[k] += sM * V;
       }
       has_old = true;
     }
