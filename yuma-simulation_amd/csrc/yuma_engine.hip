@@ -46,6 +46,14 @@
 
 #define YUMA_VERSION_STRING "yuma_hip 0.1.0 gfx950"
 
+// A/B switch: wave-uniform row scalars in the wide history scan
+#ifndef YK_WIDE_LDS_PAD
+#define YK_WIDE_LDS_PAD 0
+#endif
+#ifndef YK_ROW_UNIFORM
+#define YK_ROW_UNIFORM 0
+#endif
+
 namespace yk {
 
 constexpr int kTileM = 64;
@@ -2213,7 +2221,12 @@ __global__ __launch_bounds__(BS) void k_bonds_elem(BondArgs A) {
     const long long slice = (long long)t * N + n;
 #pragma unroll
     for (int i = 0; i < R; ++i) {
-      const int rr = min(row0 + G * i, V - 1);
+      int rr = min(row0 + G * i, V - 1);
+#if YK_ROW_UNIFORM
+      // a wave covers one row when LPR >= 64: the row scalars become
+      // wave-uniform loads
+      if (LPR >= 64) rr = __builtin_amdgcn_readfirstlane(rr);
+#endif
       load4c<VEC>(A.W + (A.wsh ? (long long)t : slice) * VM, rr, V, m, M, rw[k][i]);
       rd[k][i] = A.rsd[slice * V + rr];
       rsn[k][i] = A.sn[slice * V + rr];
@@ -3021,6 +3034,10 @@ int launch_bonds_colnorm(RowCfg rc, hipStream_t st, yk::BondArgs& A) {
 #endif
 // scenarios per block of the shared-input scan (k_bonds_grp); 1 = one
 // scenario per block (k_bonds_elem), the A/B baseline
+// epochs in flight of the wide history scan
+#ifndef YK_WIDE_P
+#define YK_WIDE_P 2
+#endif
 #ifndef YK_SCAN_GROUP
 #define YK_SCAN_GROUP 2
 #endif
@@ -3031,6 +3048,13 @@ int launch_elem_shape(hipStream_t st, yk::BondArgs& A) {
   A.rowblocks = (A.V + G * R - 1) / (G * R);
   A.cblocks = (A.M + CB - 1) / CB;
   const long long nblocks = (long long)A.N * A.rowblocks * A.cblocks;
+#if YK_WIDE_LDS_PAD
+  if (CB >= 1024) {  // A/B: dynamic LDS that leaves room for one block per CU
+    hipLaunchKernelGGL((yk::k_bonds_elem<VARIANT, R, VEC, P, VECI, NT, BS, CB, DPL>), dim3(nblocks),
+                       dim3(BS), YK_WIDE_LDS_PAD, st, A);
+    return DPL;
+  }
+#endif
   YK_LAUNCH((yk::k_bonds_elem<VARIANT, R, VEC, P, VECI, NT, BS, CB, DPL>), nblocks, BS, st, A);
   return DPL;
 }
@@ -3039,7 +3063,7 @@ int launch_bonds_elem(hipStream_t st, yk::BondArgs& A) {
   const bool hist = A.B_hist != nullptr;
   if constexpr (VEC) {
     if (hist && YK_WIDE_SCAN && A.M >= 1024)
-      return launch_elem_shape<VARIANT, 2, true, 2, true, true, 512, 1024, yk::DP_VT>(st, A);
+      return launch_elem_shape<VARIANT, 2, true, YK_WIDE_P, true, true, 512, 1024, yk::DP_VT>(st, A);
   }
   if constexpr (VEC) {
     if (A.wsh && A.N >= 2 && YK_SCAN_GROUP > 1) {  // a sweep over one input trajectory
