@@ -312,3 +312,39 @@ def test_bench_consensus_classes():
     assert bench.consensus_classes(params) == 16
     params[3].flags |= engine.FLAG_NO_HIST  # the histogram switch splits a class
     assert bench.consensus_classes(params) == 17
+
+
+def _grp_omba(ba_param: float, omba_param: float) -> np.float32:
+    """k_bonds_grp's operand for a fixed-alpha scenario (YK_GRP_CORR):
+    (1 - bond_alpha) + corr, corr = one_minus_bond_alpha - (1 - bond_alpha),
+    a NaN corr (bond_alpha = +-inf) replaced by 0, all in fp32."""
+    one = np.float32(1.0)
+    ba, omba = np.float32(ba_param), np.float32(omba_param)
+    with np.errstate(invalid="ignore", over="ignore"):
+        x = one - ba
+        corr = omba - x
+        if corr != corr:
+            corr = np.float32(0.0)
+        return x + corr
+
+
+def test_grp_one_minus_alpha_correction():
+    """The sweep scan rebuilds one_minus_bond_alpha = f32(1 - bond_alpha)
+    (double, engine.make_params) from f32(bond_alpha) bit for bit, for every
+    bond_alpha a YumaConfig can carry (yumas.py:566-575 uses 1 - bond_alpha)."""
+    rng = np.random.default_rng(7)
+    alphas = list(rng.random(200_000)) + list(rng.random(20_000) * 1e-6) + list(1 - rng.random(20_000) * 1e-6)
+    alphas += list(10.0 ** rng.uniform(-45, 40, 20_000)) + list(-(10.0 ** rng.uniform(-45, 40, 5_000)))
+    alphas += [0.0, -0.0, 1.0, 0.5, 0.1, 0.9, 0.025, 1e-9, 1 - 1e-9, 1 - 2**-24, 1 - 2**-25, 1 + 2**-23,
+               2**-126, 2**-149, 3.4e38, 1e39, -1e39, float("inf"), float("-inf")]
+    from bench import SWEEP_BOND_ALPHA  # the c3 grid's bond_alpha values
+    alphas += list(SWEEP_BOND_ALPHA)
+    bad = []
+    for a in alphas:
+        cfg = Y.YumaConfig(yuma_params=Y.YumaParams(bond_alpha=float(a)))
+        p = engine.make_params(engine.VARIANT_YUMA4, cfg)
+        got = _grp_omba(p.bond_alpha, p.one_minus_bond_alpha)
+        want = np.float32(p.one_minus_bond_alpha)
+        if got.view(np.uint32) != want.view(np.uint32):
+            bad.append((a, float(got), float(want)))
+    assert not bad, bad[:5]

@@ -47,6 +47,12 @@
 #define YUMA_VERSION_STRING "yuma_hip 0.1.0 gfx950"
 
 // A/B switch: wave-uniform row scalars in the wide history scan
+#ifndef YK_GRP_WAVES  // minimum waves per SIMD of the sweep scan
+#define YK_GRP_WAVES 6
+#endif
+#ifndef YK_GRP_CORR
+#define YK_GRP_CORR 1
+#endif
 #ifndef YK_WIDE_LDS_PAD
 #define YK_WIDE_LDS_PAD 0
 #endif
@@ -2371,10 +2377,13 @@ __global__ __launch_bounds__(BS) void k_bonds_elem(BondArgs A) {
 // per epoch instead of 64-bit slice-index products took its SALU from 137 to
 // 38 per two epochs and its SGPR spills from 48 to 22 (9.9 -> 9.1 ms);
 // packed-pair f32 math (no gain: v_pk_* issue as two ops on gfx950) and an
-// XCD-grouped block order (9.4-9.5 ms) were tried and dropped.
+// XCD-grouped block order (9.4-9.5 ms) were tried and dropped. Fixed-alpha
+// scenarios keep bond_alpha in the liquid operand (no per-element selects,
+// YK_GRP_CORR) under a 6-waves-per-SIMD bound: 9.1 -> 8.6 ms
+// (profiles/r03/ab/c3_grp_alpha_operands.txt).
 // ---------------------------------------------------------------------------
 template <int VARIANT, int K, int R, int P>
-__global__ __launch_bounds__(256) void k_bonds_grp(BondArgs A) {
+__global__ __launch_bounds__(256, YK_GRP_WAVES) void k_bonds_grp(BondArgs A) {
   constexpr int G = 16;
   const Lay L = lay();
   const int tile = blockIdx.x % A.tiles;
@@ -2500,6 +2509,26 @@ __global__ __launch_bounds__(256) void k_bonds_grp(BondArgs A) {
   for (int kk = 0; kk < P; ++kk) fetch(kk, A.t0 + kk < A.t1);
 #pragma unroll
   for (int k = 0; k < K; ++k) fetch_s(k, true);
+#if YK_GRP_CORR
+  // Fixed-alpha scenarios: bond_alpha sits in rba for the whole scan (the
+  // per-element selects between the liquid and the fixed operands go), and
+  // one_minus_bond_alpha = (1 - bond_alpha) + p_corr. Both terms of p_corr
+  // are fp32 roundings of 1 - bond_alpha within 2^-25 of each other, so
+  // their difference is exact (Sterbenz, or one of them is 0) and adding it
+  // back to 1 - bond_alpha gives one_minus_bond_alpha bit for bit
+  // (tests/test_engine_host.py::test_grp_one_minus_alpha_correction).
+  float p_corr[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    p_corr[k] = 0.0f;
+    if (!((liquid_mask >> k) & 1u)) {
+      p_corr[k] = p_omba[k] - (1.0f - p_ba[k]);
+      if (p_corr[k] != p_corr[k]) p_corr[k] = 0.0f;  // bond_alpha = +-inf: -+inf + 0
+#pragma unroll
+      for (int c = 0; c < 4; ++c) rba[k][c] = p_ba[k];
+    }
+  }
+#endif
 
   for (int tb = A.t0; tb < A.t1; tb += P) {
 #pragma unroll
@@ -2546,8 +2575,17 @@ __global__ __launch_bounds__(256) void k_bonds_grp(BondArgs A) {
         float bac[4], omba[4], ic[4];
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
+#if YK_GRP_CORR
+          // rba holds bond_alpha for a fixed-alpha scenario; p_corr turns
+          // 1 - rba into its (double-derived) one_minus_bond_alpha exactly
+          // and is +0 for a liquid one (see the set-up above)
+          (void)liquid;
+          bac[c] = rba[k][c];
+          omba[c] = (1.0f - rba[k][c]) + p_corr[k];
+#else
           bac[c] = liquid ? rba[k][c] : p_ba[k];
           omba[c] = liquid ? 1.0f - rba[k][c] : p_omba[k];
+#endif
           ic[c] = ri[k][c];
         }
         fetch_s(k, t + 1 < A.t1);
