@@ -47,6 +47,9 @@
 #define YUMA_VERSION_STRING "yuma_hip 0.1.0 gfx950"
 
 // A/B switch: wave-uniform row scalars in the wide history scan
+#ifndef YK_RANK_WAVES  // minimum waves per SIMD of the streaming rank
+#define YK_RANK_WAVES 1
+#endif
 #ifndef YK_GRP_WAVES  // minimum waves per SIMD of the sweep scan
 #define YK_GRP_WAVES 6
 #endif
@@ -1359,7 +1362,7 @@ __global__ __launch_bounds__(256) void k_rank_w(
 // sequentially per lane, then the 4 row groups of a wave (xor 16, 32), then
 // the 4 waves in order.
 template <bool VEC>
-__global__ __launch_bounds__(256) void k_rank_s(const float* __restrict__ W,
+__global__ __launch_bounds__(256, YK_RANK_WAVES) void k_rank_s(const float* __restrict__ W,
                                                 const float* __restrict__ rsd,
                                                 const float* __restrict__ sn,
                                                 const float* __restrict__ C, int N, int V, int M,
