@@ -47,6 +47,9 @@
 #define YUMA_VERSION_STRING "yuma_hip 0.1.0 gfx950"
 
 // A/B switch: wave-uniform row scalars in the wide history scan
+#ifndef YK_ELEM_WAVES  // minimum waves per SIMD of the one-row history-less scan
+#define YK_ELEM_WAVES 1
+#endif
 #ifndef YK_RANK_WAVES  // minimum waves per SIMD of the streaming rank
 #define YK_RANK_WAVES 1
 #endif
@@ -2187,7 +2190,7 @@ __global__ __launch_bounds__(NT) void k_bonds(BondArgs A) {
 // of each 64-miner tile is the 16-lane DPP sum of one DPP row in every shape.
 template <int VARIANT, int R, bool VEC, int P, bool VECI, bool NT = false, int BS = 256, int CB = 64,
           int DPL = DP_TV>
-__global__ __launch_bounds__(BS) void k_bonds_elem(BondArgs A) {
+__global__ __launch_bounds__(BS, (R == 1 && !NT) ? YK_ELEM_WAVES : 1) void k_bonds_elem(BondArgs A) {
   constexpr int LPR = CB / 4, G = BS / LPR;
   static_assert(CB % 64 == 0 && BS % LPR == 0, "a 16-lane DPP row must cover one 64-miner tile");
   const int cq = threadIdx.x % LPR, lane = threadIdx.x & 63;
