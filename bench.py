@@ -432,6 +432,13 @@ def engine_line(args, variant: int, params: list, W, S, world: int, dist: bool, 
     return line
 
 
+def input_seed(config: str, seed: int, rank: int) -> int:
+    """Seed of a rank's synthetic inputs: c3 sweeps ONE subnet trajectory on
+    every rank (the grid is dealt to the ranks, the subnet is not); c2
+    replicas are independent subnets, one per rank."""
+    return seed if config == "c3" else seed + 7919 * rank
+
+
 def bench_engine(args, world: int, rank: int, dist: bool) -> dict:
     """c2 (default) and c3: engine.run over E epochs of N scenarios per GPU."""
     from yuma_simulation._internal import engine, synth
@@ -453,11 +460,12 @@ def bench_engine(args, world: int, rank: int, dist: bool) -> dict:
     params = [engine.make_params(variant, c) for c in cfgs]
     liquid = any(p.liquid_mode != engine.LIQUID_OFF for p in params)
     hist = not args.no_history
-    seed = args.seed + 7919 * rank  # each rank simulates its own subnet(s)
-
     # inputs resident in HBM before timing; the c3 sweep runs every scenario
-    # over ONE subnet trajectory (shared W/S, params vary)
+    # over ONE subnet trajectory (shared W/S, params vary), the
+    # same on every rank (the 4096-point grid dealt to the ranks sweeps one
+    # subnet); c2 replicas: each rank simulates its own subnet
     shared = args.config == "c3"
+    seed = input_seed(args.config, args.seed, rank)
     Nin = 1 if shared else N
     W = engine.synth_weights(seed, E, Nin, V, M)
     S = torch.from_numpy(synth.stakes(seed, E, Nin, V)).to(dev)

@@ -203,3 +203,75 @@ def test_bench_timed_ranks_agree_on_step_count():
         assert p.exitcode == 0
     assert got[0][1] == got[1][1]  # same number of steps on both ranks
     assert got[0][2] == got[1][2]  # the max over ranks, on every rank
+
+
+# ---------------------------------------------------------------------------
+# GPU: the RCCL (nccl backend) path on the one-GPU box, world size 1
+# ---------------------------------------------------------------------------
+def _nccl_worker(port, q):
+    """A fresh process whose first GPU work is the nccl process group, as
+    bench.py's N-rank path opens it (init_process_group("nccl", device_id)).
+    Runs the wide subnet through run_wide_distributed (dist_gather's device
+    branch: RCCL all-gathers of the per-shard partials) and the scenario
+    gather of run_sharded, then the same work without the process group."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1",
+                      LOCAL_RANK="0")
+    try:
+        torch.cuda.set_device(0)
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+        from yuma_simulation._internal import engine, sharding, wide
+
+        assert dist.get_backend() == "nccl"
+        E, V, M = 4, 64, 1024
+        cfg = YumaConfig(yuma_params=YumaParams(liquid_alpha=True))
+        params = [engine.make_params(engine.VARIANT_YUMA4, cfg)]
+        W = engine.synth_weights(0x5EED0004, E, 1, V, M)
+        S = torch.from_numpy(synth.stakes(0x5EED0004, E, 1, V, period=2)).to(W.device)
+        got = wide.run_wide_distributed(engine.VARIANT_YUMA4, params, W, S, M_total=M, want_hist=True,
+                                        want=("Tv",))
+        # scenario sharding: 3 scenarios, this rank owns all; the rank-ordered
+        # gather of the per-epoch results through RCCL
+        n = 3
+        p3 = [engine.make_params(engine.VARIANT_YUMA4, c) for c in configs(n)]
+        W3 = engine.synth_weights(11, E, n, V, M)
+        S3 = torch.from_numpy(synth.stakes(11, E, n, V, period=2)).to(W3.device)
+        sh = sharding.run_sharded(engine.VARIANT_YUMA4, p3, W3, S3, n_total=n)
+        gathered = sharding._gather_scenarios(sh.Dn, [n])
+        torch.cuda.synchronize()
+        dist.destroy_process_group()
+        ref = wide.run_wide_local(engine.VARIANT_YUMA4, params, W, S, 1, want_hist=True, want=("Tv",))
+        full = engine.run(engine.VARIANT_YUMA4, p3, W3, S3)
+        torch.cuda.synchronize()
+        q.put({
+            "wide_Dn": torch.equal(got.Dn, ref.Dn),
+            "wide_C": torch.equal(got.C[0], ref.C[0]),
+            "wide_Bh": torch.equal(got.B_hist[0], ref.B_hist[0]),
+            "wide_Tv": torch.equal(got.extra["Tv"][0], ref.extra["Tv"][0]),
+            "wide_vs_unsharded": torch.equal(got.B_final[0], engine.run(
+                engine.VARIANT_YUMA4, params, W, S).B_final),
+            "sharded": all(torch.equal(getattr(sh, k), getattr(full, k)) for k in ("Dn", "C", "I", "B_final")),
+            "gather": torch.equal(gathered, full.Dn) and gathered.is_cuda,
+        })
+    except Exception as e:  # reported to the parent, which fails the test
+        import traceback
+
+        q.put({"error": f"{type(e).__name__}: {e}\n{traceback.format_exc()}"})
+
+
+@pytest.mark.gpu
+def test_rccl_world1_wide_and_scenario_gather():
+    """the nccl (RCCL) backend in a world-1 group on the
+    one-GPU box — run_wide_distributed's all-gathers of row-sum / ΣC / ΣR /
+    level / dividend / trust partials (dist_gather's device branch) and the
+    scenario gather of run_sharded — bitwise equal to the in-process shard
+    driver (run_wide_local(..., 1)), the unsharded engine and engine.run.
+    Reference reductions replaced: yumas.py:411,436,445,475-476."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_nccl_worker, args=(_free_port(), q))
+    p.start()
+    res = q.get(timeout=300)
+    p.join(timeout=60)
+    assert "error" not in res, res.get("error")
+    assert p.exitcode == 0
+    assert all(res.values()), res

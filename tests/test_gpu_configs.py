@@ -72,8 +72,8 @@ def _shared_vs_replicated_and_oracle(ids: list[int], E: int, oracle_ids: list[in
     """The launch `bench.py --config c3` times: every scenario reads ONE W/S
     trajectory (shared_inputs, yuma_run_ex YUMA_RUN_SHARED_INPUTS), no bond
     history. At 256 x 4096 that is the shared-input bond scan
-    (launch_bonds_elem: k_bonds_elem<YUMA4, R=2, VEC, P=2, VECI, NT=false>),
-    the row sums once per input epoch and the consensus / quantisation input /
+    (launch_bonds_elem: k_bonds_grp<YUMA4, K=2, R=1, P=2>, two scenarios per
+    block over one W tile), the row sums once per input epoch and the consensus / quantisation input /
     rank once per consensus class (k_classes). C, Dn, I and B_final must be
     bitwise those of the same run on W and S replicated per scenario (every
     scenario computing its own everything), and each scenario in oracle_ids
@@ -160,6 +160,36 @@ def test_c4_wide_eight_shards_matches_unsharded_and_oracle():
     assert_close(Bh[:2, 0].cpu().numpy(), o["B"], what="B vs oracle")
 
 
+def test_c4_bench_launch_without_history():
+    """the launch `bench.py --config c4` times —
+    engine.run(Yuma 3, want_hist=False) at 256 x 65536, i.e. the history-less
+    scan k_bonds_elem<YUMA3, R=1, VEC, P=4, VECI> over 64-miner tiles with
+    [slice][tile][V] dividend partials. 3 epochs: C, Dn, I and B_final bitwise
+    those of the history run (the wide history scan, [slice][V][tile]
+    partials, same summation order); 2 epochs against the oracle: C exact,
+    Dn, I and B_final within 1e-5 (yumas.py:452-476)."""
+    E, V, M = 3, 256, 65536
+    cfg = YumaConfig()
+    params = [engine.make_params(engine.VARIANT_YUMA3, cfg)]
+    seed = 0x5EED0004
+    W = engine.synth_weights(seed, E, 1, V, M)
+    S = torch.from_numpy(synth.stakes(seed, E, 1, V)).to(W.device)
+    a = engine.run(engine.VARIANT_YUMA3, params, W, S, want_hist=False)
+    b = engine.run(engine.VARIANT_YUMA3, params, W, S, want_hist=True)
+    torch.cuda.synchronize()
+    for k in ("C", "Dn", "I", "B_final"):
+        assert torch.equal(getattr(a, k), getattr(b, k)), k
+    assert torch.equal(a.B_final[0], b.B_hist[-1, 0])
+    del a, b
+    a2 = engine.run(engine.VARIANT_YUMA3, params, W[:2].contiguous(), S[:2].contiguous(), want_hist=False)
+    torch.cuda.synchronize()
+    o = orc.run("Yuma 3 (Rhef)", W[:2, 0].cpu().numpy(), S[:2, 0].cpu().numpy(), cfg)
+    np.testing.assert_array_equal(a2.C[:, 0].cpu().numpy(), o["C"])
+    assert_close(a2.Dn[:, 0].cpu().numpy(), o["Dn"], what="Dn vs oracle")
+    assert_close(a2.I[:, 0].cpu().numpy(), o["I"], what="I vs oracle")
+    assert_close(a2.B_final[0].cpu().numpy(), o["B"][-1], what="B_final vs oracle")
+
+
 def _tie_report(C_gpu, C_ref, W, S, cfg, as_double=False):
     """(mismatched columns outside the tie window, tie-window size, mismatches inside)."""
     flags = orc.tie_columns(W, S, cfg.kappa, cfg.consensus_precision, as_double)
@@ -229,15 +259,21 @@ def test_wide_float_weights_against_oracle():
     assert_close(torch.cat(got.B_hist, dim=3)[:, 0].cpu().numpy(), ref["B"], what="B")
 
 
-@pytest.mark.parametrize("variant,extra,reset,chunk,want", [
-    (engine.VARIANT_YUMA4, {"liquid_alpha": True}, None, 0, ("R", "D")),
-    (engine.VARIANT_YUMA3, {}, (3, 5), 4, ("R", "D")),
-    (engine.VARIANT_YUMA3, {}, None, 0, ("R", "D", "T", "Tv")),
-    (engine.VARIANT_YUMA2, {"liquid_alpha": True}, None, 3, ("R", "D")),
-    (engine.VARIANT_RUST, {}, None, 0, ("R", "D")),
-    (engine.VARIANT_YUMA1, {"bond_penalty": 0.5}, None, 5, ("R", "D")),
+@pytest.mark.parametrize("variant,extra,reset,chunk,want,N", [
+    (engine.VARIANT_YUMA4, {"liquid_alpha": True}, None, 0, ("R", "D"), 6),
+    (engine.VARIANT_YUMA3, {}, (3, 5), 4, ("R", "D"), 6),
+    (engine.VARIANT_YUMA3, {}, None, 0, ("R", "D", "T", "Tv"), 6),
+    (engine.VARIANT_YUMA2, {"liquid_alpha": True}, None, 3, ("R", "D"), 6),
+    (engine.VARIANT_RUST, {}, None, 0, ("R", "D"), 6),
+    (engine.VARIANT_YUMA1, {"bond_penalty": 0.5}, None, 5, ("R", "D"), 6),
+    # k_bonds_grp's fixed-alpha operand (p_corr) with the history
+    # stream, and its conditional reset reading the previous slice's C of
+    # scenario n0 + k; odd N leaves the last block one scenario (nk < K)
+    (engine.VARIANT_YUMA4, {}, None, 0, ("R", "D"), 7),
+    (engine.VARIANT_YUMA4, {}, (4, 7, "zero"), 0, ("R", "D"), 7),
+    (engine.VARIANT_YUMA4, {"liquid_alpha": True}, (2, 7, "zero"), 3, (), 5),
 ])
-def test_shared_input_sweep_equals_replicated(variant, extra, reset, chunk, want):
+def test_shared_input_sweep_equals_replicated(variant, extra, reset, chunk, want, N):
     """yuma_run_ex(YUMA_RUN_SHARED_INPUTS): N scenarios reading ONE W/S
     trajectory ([E,1,V,M]) give bitwise the results of the same run on W and S
     replicated per scenario — consensus, bonds and their history, dividends,
@@ -246,10 +282,15 @@ def test_shared_input_sweep_equals_replicated(variant, extra, reset, chunk, want
     across scenarios (three consensus classes of two, k_classes: the second of
     each takes the first's consensus, quantisation input and rank); with P / T
     / T_v requested every scenario computes its own."""
-    E, N, V, M = 10, 6, 64, 512
+    E, V, M = 10, 64, 512
     seed = 0x5EED0003
     W1 = engine.synth_weights(seed, E, 1, V, M)
     S1 = torch.from_numpy(synth.stakes(seed, E, 1, V, period=3)).to(W1.device)
+    zero_reset = reset is not None and len(reset) > 2
+    if zero_reset:
+        # an all-zero miner column quantises to C = 0, so the conditional
+        # reset (simulation_utils.py:79-85) fires the epoch after
+        W1[reset[0] - 1, ..., reset[1]] = 0.0
     cfgs = []
     for i in range(N):
         sim = {k: v for k, v in extra.items() if k in ("bond_penalty",)}
@@ -258,7 +299,8 @@ def test_shared_input_sweep_equals_replicated(variant, extra, reset, chunk, want
                                yuma_params=YumaParams(bond_alpha=0.05 + 0.05 * i, **prm)))
     kw = {}
     if reset is not None:
-        kw = {"reset_mode": engine.RESET_ALWAYS, "reset_epoch": reset[0], "reset_index": reset[1],
+        mode = engine.RESET_IF_ZERO_CONSENSUS if zero_reset else engine.RESET_ALWAYS
+        kw = {"reset_mode": mode, "reset_epoch": reset[0], "reset_index": reset[1],
               "n_miners": M, "n_epochs": E}
     params = [engine.make_params(variant, c, **kw) for c in cfgs]
     a = engine.run(variant, params, W1, S1, want_hist=True, want=want, chunk_epochs=chunk,
@@ -273,10 +315,21 @@ def test_shared_input_sweep_equals_replicated(variant, extra, reset, chunk, want
     version = {engine.VARIANT_RUST: "Yuma 0 (subtensor)", engine.VARIANT_YUMA1: "Yuma 1 (paper)",
                engine.VARIANT_YUMA2: "Yuma 2 (Adrian-Fish)", engine.VARIANT_YUMA3: "Yuma 3 (Rhef)",
                engine.VARIANT_YUMA4: "Yuma 4 (Rhef+relative bonds)"}[variant]
-    if reset is None:
-        ref = orc.run(version, W1[:, 0].cpu().numpy(), S1[:, 0].cpu().numpy(), cfgs[0])
+    if zero_reset:
+        assert (a.C[reset[0] - 1, :, reset[1]] == 0).all()
+    if reset is None or zero_reset:
+        rk = {}
+        if zero_reset:
+            rk = {"reset_epoch": reset[0], "reset_index": reset[1]}
+        ref = orc.run(version, W1[:, 0].cpu().numpy(), S1[:, 0].cpu().numpy(), cfgs[0], **rk)
         np.testing.assert_array_equal(a.C[:, 0].cpu().numpy(), ref["C"])
         assert_close(a.Dn[:, 0].cpu().numpy(), ref["Dn"], what="shared sweep Dn vs oracle")
+        assert_close(a.B_hist[:, 0].cpu().numpy(), ref["B"], what="shared sweep B vs oracle")
+        if zero_reset:  # the reset fired: without it the column's bonds differ
+            ref0 = orc.run(version, W1[:, 0].cpu().numpy(), S1[:, 0].cpu().numpy(), cfgs[0])
+            e, j = reset[0], reset[1]
+            assert not np.allclose(ref0["B"][e][:, j], ref["B"][e][:, j])
+            np.testing.assert_array_equal(ref["B"][e - 1][:, j] > 0, ref0["B"][e - 1][:, j] > 0)
 
 
 def bench_sim(**kw):

@@ -164,14 +164,19 @@ def test_reset_packing_equals_reference_statement():
     in torch (simulation_utils.py:63-64 Yuma 3.1, :68-74 / :79-85 Yuma 3.2 / 4
     with scw all zero so the condition holds wherever it is defined): for
     every epoch of the run, which columns are zeroed, or the error raised.
-    Covers float / bool / numpy epochs and bool / numpy indices."""
+    Covers float / bool / numpy epochs, 0-d and one-element tensors / arrays
+    (truthy like their element), tensors / arrays of other sizes
+    (no truth value: the reference raises) and bool / numpy indices."""
     M, E = 5, 6
 
     def reference(mode, e_ref, idx):
         out = {}
         for epoch in range(1, E):  # B_state exists from epoch 1 on
-            if not epoch == e_ref:
-                continue
+            try:
+                if not epoch == e_ref:
+                    continue
+            except (RuntimeError, ValueError):  # a tensor / array without a truth value
+                return "raise"
             B = torch.ones(2, M)
             if mode == engine.RESET_IF_ZERO_CONSENSUS:
                 try:
@@ -190,14 +195,16 @@ def test_reset_packing_equals_reference_statement():
         try:
             p = engine.make_params(engine.VARIANT_YUMA3, Y.YumaConfig(), reset_mode=mode, reset_epoch=e_ref,
                                    reset_index=idx, n_miners=M, n_epochs=E)
-        except RuntimeError:
+        except (RuntimeError, ValueError):
             return "raise"
         if p.reset_mode == engine.RESET_NONE:
             return {}
         cols = range(M) if p.flags & engine.FLAG_RESET_ALL_COLUMNS else [p.reset_index]
         return {p.reset_epoch: frozenset(cols)}
 
-    epochs = [3, 3.0, 3.5, True, False, np.int64(2), 0, -1, 6, "3", None]
+    epochs = [3, 3.0, 3.5, True, False, np.int64(2), 0, -1, 6, "3", None,
+              torch.tensor(3), torch.tensor([3]), torch.tensor(3.0), torch.tensor(3.5), torch.tensor(True),
+              np.array(2), np.array([4.0]), torch.tensor([3, 4]), np.array([3, 4]), torch.tensor([]), np.array([])]
     indices = [2, -1, np.int64(4), True, False, None]
     for mode in (engine.RESET_ALWAYS, engine.RESET_IF_ZERO_CONSENSUS):
         for e_ref in epochs:
@@ -314,8 +321,22 @@ def test_bench_consensus_classes():
     assert bench.consensus_classes(params) == 17
 
 
+def test_bench_input_seed_per_config():
+    """an N-rank c3 line sweeps ONE subnet trajectory (every rank
+    the same inputs, its own share of the grid); c2 replicas are independent
+    subnets, one seed per rank."""
+    import sys
+
+    sys.path.insert(0, ROOT)
+    import bench
+
+    assert {bench.input_seed("c3", 0x5EED0003, r) for r in range(8)} == {0x5EED0003}
+    assert len({bench.input_seed("c2", 0x5EED0002, r) for r in range(8)}) == 8
+    assert bench.input_seed("c2", 0x5EED0002, 0) == 0x5EED0002
+
+
 def _grp_omba(ba_param: float, omba_param: float) -> np.float32:
-    """k_bonds_grp's operand for a fixed-alpha scenario (YK_GRP_CORR):
+    """k_bonds_grp's operand for a fixed-alpha scenario (p_corr):
     (1 - bond_alpha) + corr, corr = one_minus_bond_alpha - (1 - bond_alpha),
     a NaN corr (bond_alpha = +-inf) replaced by 0, all in fp32."""
     one = np.float32(1.0)

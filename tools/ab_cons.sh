@@ -1,5 +1,5 @@
 #!/bin/bash
-# A/B of consensus kernels (ablib/cp*.so built with -DYK_CONS_PIPE=K): per-phase
+# A/B of consensus kernels (ablib/*.so from tools/ab_build.py): per-phase
 # device time of the c2 Yuma 3 workload, two rounds.
 export TMPDIR=/tmp
 for rep in 1 2; do

@@ -1,0 +1,24 @@
+"""Patch sets for tools/ab_build.py: PATCHES[name] = [(old, new[, count]), ...]
+applied to yuma-simulation_amd/csrc/yuma_engine.hip. Timing-only builds are
+named diag_* (wrong results by design; never used for parity)."""
+
+PATCHES = {
+    # k_consensus_w: W loads + division only, no prerank / search (round 3,
+    # profiles/r03/ab/consensus_lds_stage_diag.txt "d1")
+    "diag_cons_loadonly": [(
+        "  const LdsRows s{&rl[0][0], L.wave * 48 * R + 16 * R + L.rg};\n  if (Pout",
+        "  const LdsRows s{&rl[0][0], L.wave * 48 * R + 16 * R + L.rg};\n"
+        "  {\n    float t = 0.0f;\n    for (int i = 0; i < R; ++i) for (int c = 0; c < 4; ++c) t = t + wn[i][c];\n"
+        "    if (t == 1234.5f) craw[slice * M + m] = t;\n    return;\n  }\n  if (Pout")],
+    # k_consensus_w without the W read: weights made up from the indices ("d2")
+    "diag_cons_noload": [(
+        "  if (allfull) {\n    const unsigned o0 = (unsigned)rg * (unsigned)M + (unsigned)m, st = 16u * (unsigned)M;\n"
+        "#pragma unroll\n    for (int i = 0; i < R; ++i) {\n      const float4 t = *reinterpret_cast<const float4*>(Ws + (o0 + (unsigned)i * st));\n"
+        "      wn[i][0] = t.x;\n      wn[i][1] = t.y;\n      wn[i][2] = t.z;\n      wn[i][3] = t.w;\n    }\n  } else {",
+        "  if (allfull) {\n    for (int i = 0; i < R; ++i)\n      for (int c = 0; c < 4; ++c)"
+        " wn[i][c] = (float)(((rg + 16 * i) * 37 + (m + c) * 11) & 4095);\n  } else {")],
+    # k_bonds_elem without the dividend-partial stores (profiles/r03/ab/scan_partials_diag.txt)
+    "diag_no_dp": [(
+        "        d = wsum16(d);  // sum_row16's xor-butterfly tree, on DPP\n        if",
+        "        d = wsum16(d);  // sum_row16's xor-butterfly tree, on DPP\n        if (d == 1.2345e-37f)\n        if")],
+}

@@ -1,5 +1,5 @@
 #!/bin/bash
-# A/B of bond-scan shapes (ablib/w*.so built with -DYK_WIDE_SCAN=k): per-phase
+# A/B of bond-scan shapes (ablib/*.so from tools/ab_build.py): per-phase
 # device time of the c2 workloads with the bond history (Yuma 3, Yuma 4
 # liquid), two rounds so box drift shows.
 export TMPDIR=/tmp

@@ -46,25 +46,8 @@
 
 #define YUMA_VERSION_STRING "yuma_hip 0.1.0 gfx950"
 
-// A/B switch: wave-uniform row scalars in the wide history scan
-#ifndef YK_ELEM_WAVES  // minimum waves per SIMD of the one-row history-less scan
-#define YK_ELEM_WAVES 1
-#endif
-#ifndef YK_RANK_WAVES  // minimum waves per SIMD of the streaming rank
-#define YK_RANK_WAVES 1
-#endif
-#ifndef YK_GRP_WAVES  // minimum waves per SIMD of the sweep scan
-#define YK_GRP_WAVES 6
-#endif
-#ifndef YK_GRP_CORR
-#define YK_GRP_CORR 1
-#endif
-#ifndef YK_WIDE_LDS_PAD
-#define YK_WIDE_LDS_PAD 0
-#endif
-#ifndef YK_ROW_UNIFORM
-#define YK_ROW_UNIFORM 0
-#endif
+// Kernel variants are A/B-tested from patched copies of this file
+// (tools/ab_build.py), so the product source carries no build switches.
 
 namespace yk {
 
@@ -826,14 +809,6 @@ __device__ __forceinline__ void load_norm_w_lds(const float* __restrict__ Ws, co
   }
   const bool full = rg + 16 * (R - 1) < V && m + 3 < M;
   const bool allfull = VEC && __all(full) && (long long)V * M < (1ll << 30);
-#ifdef YK_DIAG_CONS_NOLOAD  // timing-only: weights made up from the indices, no W read
-  if (allfull) {
-#pragma unroll
-    for (int i = 0; i < R; ++i)
-#pragma unroll
-      for (int c = 0; c < 4; ++c) wn[i][c] = (float)(((rg + 16 * i) * 37 + (m + c) * 11) & 4095);
-  } else
-#else
   if (allfull) {
     const unsigned o0 = (unsigned)rg * (unsigned)M + (unsigned)m, st = 16u * (unsigned)M;
 #pragma unroll
@@ -844,9 +819,7 @@ __device__ __forceinline__ void load_norm_w_lds(const float* __restrict__ Ws, co
       wn[i][2] = t.z;
       wn[i][3] = t.w;
     }
-  } else
-#endif
-  {
+  } else {
 #pragma unroll
     for (int i = 0; i < R; ++i) load4c<VEC>(Ws, rg + 16 * i, V, m, M, wn[i]);
   }
@@ -1217,17 +1190,6 @@ __global__ __launch_bounds__(256, 4) void k_consensus_w(const float* __restrict_
   load_norm_w_lds<R, VEC>(W + in_slice(slice, N, wsh) * (long long)V * M, rsd + slice * V,
                           sn + slice * V, rl[L.wave], V, M, m, L.rg, L.lane, wn);
   const LdsRows s{&rl[0][0], L.wave * 48 * R + 16 * R + L.rg};
-#ifdef YK_DIAG_CONS_LOADONLY  // timing-only: the W loads and division, nothing else
-  {
-    float t = 0.0f;
-#pragma unroll
-    for (int i = 0; i < R; ++i)
-#pragma unroll
-      for (int c = 0; c < 4; ++c) t = t + wn[i][c];
-    if (t == 1234.5f) craw[slice * M + m] = t;
-    return;
-  }
-#endif
   if (Pout != nullptr) prerank_store<R>(wn, s, L, m, M, Pout + slice * M);
   int hi_k[4];
   const yuma_params_t& p = prm[n];
@@ -1365,7 +1327,7 @@ __global__ __launch_bounds__(256) void k_rank_w(
 // sequentially per lane, then the 4 row groups of a wave (xor 16, 32), then
 // the 4 waves in order.
 template <bool VEC>
-__global__ __launch_bounds__(256, YK_RANK_WAVES) void k_rank_s(const float* __restrict__ W,
+__global__ __launch_bounds__(256, 1) void k_rank_s(const float* __restrict__ W,
                                                 const float* __restrict__ rsd,
                                                 const float* __restrict__ sn,
                                                 const float* __restrict__ C, int N, int V, int M,
@@ -2190,7 +2152,7 @@ __global__ __launch_bounds__(NT) void k_bonds(BondArgs A) {
 // of each 64-miner tile is the 16-lane DPP sum of one DPP row in every shape.
 template <int VARIANT, int R, bool VEC, int P, bool VECI, bool NT = false, int BS = 256, int CB = 64,
           int DPL = DP_TV>
-__global__ __launch_bounds__(BS, (R == 1 && !NT) ? YK_ELEM_WAVES : 1) void k_bonds_elem(BondArgs A) {
+__global__ __launch_bounds__(BS, 1) void k_bonds_elem(BondArgs A) {
   constexpr int LPR = CB / 4, G = BS / LPR;
   static_assert(CB % 64 == 0 && BS % LPR == 0, "a 16-lane DPP row must cover one 64-miner tile");
   const int cq = threadIdx.x % LPR, lane = threadIdx.x & 63;
@@ -2233,12 +2195,7 @@ __global__ __launch_bounds__(BS, (R == 1 && !NT) ? YK_ELEM_WAVES : 1) void k_bon
     const long long slice = (long long)t * N + n;
 #pragma unroll
     for (int i = 0; i < R; ++i) {
-      int rr = min(row0 + G * i, V - 1);
-#if YK_ROW_UNIFORM
-      // a wave covers one row when LPR >= 64: the row scalars become
-      // wave-uniform loads
-      if (LPR >= 64) rr = __builtin_amdgcn_readfirstlane(rr);
-#endif
+      const int rr = min(row0 + G * i, V - 1);
       load4c<VEC>(A.W + (A.wsh ? (long long)t : slice) * VM, rr, V, m, M, rw[k][i]);
       rd[k][i] = A.rsd[slice * V + rr];
       rsn[k][i] = A.sn[slice * V + rr];
@@ -2350,9 +2307,6 @@ __global__ __launch_bounds__(BS, (R == 1 && !NT) ? YK_ELEM_WAVES : 1) void k_bon
             if (m + c < M) d = d + B[i][c] * ri[k][c];
         }
         d = wsum16(d);  // sum_row16's xor-butterfly tree, on DPP
-#ifdef YK_DIAG_NO_DP  // timing-only build: the partials' stores left out (wrong dividends)
-        if (d == 1.2345e-37f)
-#endif
         if ((lane & 15) == 0 && row < V && tile < A.tiles)
           A.dpart[dp_index(DPL, slice, tile, row, A.tiles, V)] = d;
       }
@@ -2384,12 +2338,13 @@ __global__ __launch_bounds__(BS, (R == 1 && !NT) ? YK_ELEM_WAVES : 1) void k_bon
 // 38 per two epochs and its SGPR spills from 48 to 22 (9.9 -> 9.1 ms);
 // packed-pair f32 math (no gain: v_pk_* issue as two ops on gfx950) and an
 // XCD-grouped block order (9.4-9.5 ms) were tried and dropped. Fixed-alpha
-// scenarios keep bond_alpha in the liquid operand (no per-element selects,
-// YK_GRP_CORR) under a 6-waves-per-SIMD bound: 9.1 -> 8.6 ms
+// scenarios keep bond_alpha in the liquid operand (no per-element selects)
+// under a 6-waves-per-SIMD bound: 9.1 -> 8.6 ms
 // (profiles/r03/ab/c3_grp_alpha_operands.txt).
 // ---------------------------------------------------------------------------
+constexpr int kGrpWaves = 6;  // minimum waves per SIMD of the sweep scan
 template <int VARIANT, int K, int R, int P>
-__global__ __launch_bounds__(256, YK_GRP_WAVES) void k_bonds_grp(BondArgs A) {
+__global__ __launch_bounds__(256, kGrpWaves) void k_bonds_grp(BondArgs A) {
   constexpr int G = 16;
   const Lay L = lay();
   const int tile = blockIdx.x % A.tiles;
@@ -2515,14 +2470,13 @@ __global__ __launch_bounds__(256, YK_GRP_WAVES) void k_bonds_grp(BondArgs A) {
   for (int kk = 0; kk < P; ++kk) fetch(kk, A.t0 + kk < A.t1);
 #pragma unroll
   for (int k = 0; k < K; ++k) fetch_s(k, true);
-#if YK_GRP_CORR
   // Fixed-alpha scenarios: bond_alpha sits in rba for the whole scan (the
   // per-element selects between the liquid and the fixed operands go), and
   // one_minus_bond_alpha = (1 - bond_alpha) + p_corr. Both terms of p_corr
   // are fp32 roundings of 1 - bond_alpha within 2^-25 of each other, so
   // their difference is exact (Sterbenz, or one of them is 0) and adding it
   // back to 1 - bond_alpha gives one_minus_bond_alpha bit for bit
-  // (tests/test_engine_host.py::test_grp_one_minus_alpha_correction).
+  // (tests/test_host.py::test_grp_one_minus_alpha_correction).
   float p_corr[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) {
@@ -2534,7 +2488,6 @@ __global__ __launch_bounds__(256, YK_GRP_WAVES) void k_bonds_grp(BondArgs A) {
       for (int c = 0; c < 4; ++c) rba[k][c] = p_ba[k];
     }
   }
-#endif
 
   for (int tb = A.t0; tb < A.t1; tb += P) {
 #pragma unroll
@@ -2561,7 +2514,6 @@ __global__ __launch_bounds__(256, YK_GRP_WAVES) void k_bonds_grp(BondArgs A) {
 #pragma unroll
       for (int k = 0; k < K; ++k) {
         if (k >= nk) break;
-        const bool liquid = (liquid_mask >> k) & 1u;
         const bool reset_all = (rall_mask >> k) & 1u;
         const int reset_mode = p_rmode[k], reset_index = p_rindex[k];
         if (__builtin_expect(t == p_repoch[k] && has_old && reset_mode != YUMA_RESET_NONE &&
@@ -2581,17 +2533,11 @@ __global__ __launch_bounds__(256, YK_GRP_WAVES) void k_bonds_grp(BondArgs A) {
         float bac[4], omba[4], ic[4];
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
-#if YK_GRP_CORR
           // rba holds bond_alpha for a fixed-alpha scenario; p_corr turns
           // 1 - rba into its (double-derived) one_minus_bond_alpha exactly
           // and is +0 for a liquid one (see the set-up above)
-          (void)liquid;
           bac[c] = rba[k][c];
           omba[c] = (1.0f - rba[k][c]) + p_corr[k];
-#else
-          bac[c] = liquid ? rba[k][c] : p_ba[k];
-          omba[c] = liquid ? 1.0f - rba[k][c] : p_omba[k];
-#endif
           ic[c] = ri[k][c];
         }
         fetch_s(k, t + 1 < A.t1);
@@ -3071,20 +3017,11 @@ int launch_bonds_colnorm(RowCfg rc, hipStream_t st, yk::BondArgs& A) {
 // in the engine c2 Yuma 3 bonds 1.66-1.72 -> 1.54-1.58 ms). Without the
 // history the same shapes lose (c2 1.05 -> 1.07-1.69 ms, c4 1.63 -> 1.63-1.84,
 // the c3 sweep 10.2 -> 10.6-14.7 ms: profiles/r03/ab/scan_shapes_nohist.txt).
-// (YK_WIDE_SCAN=0 builds the 64-miner-tile scan everywhere: the A/B
-// harness, tools/ab_scan.sh)
-#ifndef YK_WIDE_SCAN
-#define YK_WIDE_SCAN 1
-#endif
-// scenarios per block of the shared-input scan (k_bonds_grp); 1 = one
-// scenario per block (k_bonds_elem), the A/B baseline
-// epochs in flight of the wide history scan
-#ifndef YK_WIDE_P
-#define YK_WIDE_P 2
-#endif
-#ifndef YK_SCAN_GROUP
-#define YK_SCAN_GROUP 2
-#endif
+// Sweeps over one shared input trajectory run k_bonds_grp with K = 2
+// scenarios per block (K = 1 / 3 / 4 / 8 measured slower,
+// profiles/r03/ab/c3_scan_group_k.txt).
+constexpr int kWideP = 2;      // epochs in flight of the wide history scan
+constexpr int kScanGroup = 2;  // scenarios per block of the shared-input scan
 int bonds_rows(bool vec, bool hist, bool wsh) { return vec && (hist || wsh) ? 2 : 1; }
 template <int VARIANT, int R, bool VEC, int P, bool VECI, bool NT, int BS, int CB, int DPL>
 int launch_elem_shape(hipStream_t st, yk::BondArgs& A) {
@@ -3092,13 +3029,6 @@ int launch_elem_shape(hipStream_t st, yk::BondArgs& A) {
   A.rowblocks = (A.V + G * R - 1) / (G * R);
   A.cblocks = (A.M + CB - 1) / CB;
   const long long nblocks = (long long)A.N * A.rowblocks * A.cblocks;
-#if YK_WIDE_LDS_PAD
-  if (CB >= 1024) {  // A/B: dynamic LDS that leaves room for one block per CU
-    hipLaunchKernelGGL((yk::k_bonds_elem<VARIANT, R, VEC, P, VECI, NT, BS, CB, DPL>), dim3(nblocks),
-                       dim3(BS), YK_WIDE_LDS_PAD, st, A);
-    return DPL;
-  }
-#endif
   YK_LAUNCH((yk::k_bonds_elem<VARIANT, R, VEC, P, VECI, NT, BS, CB, DPL>), nblocks, BS, st, A);
   return DPL;
 }
@@ -3106,12 +3036,12 @@ template <int VARIANT, bool VEC>
 int launch_bonds_elem(hipStream_t st, yk::BondArgs& A) {
   const bool hist = A.B_hist != nullptr;
   if constexpr (VEC) {
-    if (hist && YK_WIDE_SCAN && A.M >= 1024)
-      return launch_elem_shape<VARIANT, 2, true, YK_WIDE_P, true, true, 512, 1024, yk::DP_VT>(st, A);
+    if (hist && A.M >= 1024)
+      return launch_elem_shape<VARIANT, 2, true, kWideP, true, true, 512, 1024, yk::DP_VT>(st, A);
   }
   if constexpr (VEC) {
-    if (A.wsh && A.N >= 2 && YK_SCAN_GROUP > 1) {  // a sweep over one input trajectory
-      constexpr int K = YK_SCAN_GROUP, R = 1;
+    if (A.wsh && A.N >= 2) {  // a sweep over one input trajectory
+      constexpr int K = kScanGroup, R = 1;
       A.rowblocks = (A.V + 16 * R - 1) / (16 * R);
       A.cblocks = A.tiles;
       const long long nblocks = (long long)((A.N + K - 1) / K) * A.rowblocks * A.tiles;

@@ -276,11 +276,27 @@ def make_params(variant: int, config, *, maxint: int = 2**64 - 1, reset_mode: in
     return p
 
 
+class _NoTruthValue(Exception):
+    """reset_bonds_epoch is a tensor / array whose `epoch == e` has no truth value."""
+
+    def __init__(self, value):
+        super().__init__()
+        self.value = value
+
+
 def _reset_epoch_value(reset_epoch) -> int | None:
     """The int epoch e at which the reference's `epoch == case.reset_bonds_epoch`
     (simulation_utils.py:63,70,81; epoch an int from range()) holds, or None
     when it never does: ints and bools (True == 1) as themselves, a float only
-    when integral (20.0 == 20, 20.5 never), anything else never."""
+    when integral (20.0 == 20, 20.5 never), a one-element tensor or array as
+    its element (`epoch == tensor(20)` is a truthy tensor), anything else
+    never. Tensors and arrays of any other size have no truth value: the
+    caller raises the reference's own error when the statement is reached."""
+    if isinstance(reset_epoch, (torch.Tensor, np.ndarray)):
+        n = reset_epoch.numel() if isinstance(reset_epoch, torch.Tensor) else reset_epoch.size
+        if n != 1:
+            raise _NoTruthValue(reset_epoch)
+        return _reset_epoch_value(reset_epoch.item())
     if isinstance(reset_epoch, (bool, np.bool_, numbers.Integral)):
         return int(reset_epoch)
     if isinstance(reset_epoch, numbers.Real):
@@ -314,7 +330,12 @@ def _pack_reset(p: YumaParamsC, reset_mode: int, reset_epoch, reset_index, n_min
     p.reset_index = 0
     if reset_mode == RESET_NONE or reset_epoch is None:
         return
-    epoch = _reset_epoch_value(reset_epoch)
+    try:
+        epoch = _reset_epoch_value(reset_epoch)
+    except _NoTruthValue as e:
+        if n_epochs is None or n_epochs >= 2:  # reached at epoch 1: the reference's own error
+            bool(1 == e.value)
+        return
     if epoch is None or epoch < 1 or (n_epochs is not None and epoch >= n_epochs):
         return  # the statement never runs
     if not -2**31 <= epoch < 2**31:
