@@ -272,6 +272,10 @@ def test_wide_float_weights_against_oracle():
     (engine.VARIANT_YUMA4, {}, None, 0, ("R", "D"), 7),
     (engine.VARIANT_YUMA4, {}, (4, 7, "zero"), 0, ("R", "D"), 7),
     (engine.VARIANT_YUMA4, {"liquid_alpha": True}, (2, 7, "zero"), 3, (), 5),
+    # the column-normalised strip scan (k_bonds_cn: V > 64), padded rows
+    (engine.VARIANT_RUST, {"liquid_alpha": True}, None, 4, ("R", "D"), (5, 200)),
+    (engine.VARIANT_YUMA1, {}, None, 0, ("R", "D", "T", "Tv"), (6, 130)),
+    (engine.VARIANT_YUMA2, {}, None, 3, ("R", "D"), (4, 256)),
 ])
 def test_shared_input_sweep_equals_replicated(variant, extra, reset, chunk, want, N):
     """yuma_run_ex(YUMA_RUN_SHARED_INPUTS): N scenarios reading ONE W/S
@@ -283,6 +287,8 @@ def test_shared_input_sweep_equals_replicated(variant, extra, reset, chunk, want
     each takes the first's consensus, quantisation input and rank); with P / T
     / T_v requested every scenario computes its own."""
     E, V, M = 10, 64, 512
+    if isinstance(N, tuple):
+        N, V = N
     seed = 0x5EED0003
     W1 = engine.synth_weights(seed, E, 1, V, M)
     S1 = torch.from_numpy(synth.stakes(seed, E, 1, V, period=3)).to(W1.device)

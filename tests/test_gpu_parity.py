@@ -361,13 +361,17 @@ def test_multi_epoch_vs_oracle_and_chunk_invariance(variant):
     assert np.all(tot <= 1.0 + 1e-5) and np.all(tot > 0.5)
 
 
-def test_batched_scenarios_equal_individual_runs():
-    """N scenarios in one launch == each alone (bitwise), params differing."""
-    E, N, V, M = 6, 5, 64, 1000  # M % 4 == 0 but not a multiple of 64
+@pytest.mark.parametrize("V,vids", [(64, (engine.VARIANT_YUMA1, engine.VARIANT_YUMA4)),
+                                     (160, (engine.VARIANT_RUST, engine.VARIANT_YUMA1, engine.VARIANT_YUMA2))])
+def test_batched_scenarios_equal_individual_runs(V, vids):
+    """N scenarios in one launch == each alone (bitwise), params differing.
+    V = 160: the column-normalised strip scan (k_bonds_cn) with padded rows
+    and a half-filled last 16-miner strip."""
+    E, N, M = 6, 5, 1000  # M % 4 == 0 but not a multiple of 64 (nor of 16)
     W = synth.weights(77, E, N, V, M)
     S = synth.stakes(77, E, N, V, period=3)
     cfgs = [config_from({"kappa": 0.3 + 0.1 * n, "liquid_alpha": n % 2 == 1}) for n in range(N)]
-    for vid in (engine.VARIANT_YUMA1, engine.VARIANT_YUMA4):
+    for vid in vids:
         prm = [engine.make_params(vid, c) for c in cfgs]
         full = engine.run(vid, prm, torch.from_numpy(W), torch.from_numpy(S), want_hist=True)
         for n in range(N):

@@ -261,3 +261,22 @@ def test_wide_distributed_two_ranks(name):
                                   ref.B_hist.cpu().numpy())
     assert_close(got[0][0], ref.Dn.cpu().numpy(), what="Dn")
     assert_close(np.concatenate([got[r][2] for r in range(world)], axis=2), ref.I.cpu().numpy(), what="I")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["rust", "yuma1_liquid", "yuma2"])
+def test_wide_local_strip_scan_matches_unsharded(name):
+    """The column-normalised strip scan (k_bonds_cn, subnets above 64
+    validators) under miner-column shards: the bond recurrence normalises
+    over validators only, so consensus and the bonds are bitwise those of the
+    unsharded run; dividends add the shards' strip partials in shard order
+    (within 1e-5)."""
+    variant, par = CASES[name]
+    Ew, Vw, Mw = 5, 136, 400
+    W = torch.from_numpy(synth.weights(0x5EED9, Ew, 2, Vw, Mw))
+    S = torch.from_numpy(synth.stakes(0x5EED9, Ew, 2, Vw, period=2))
+    params = _params(variant, par, 2)
+    ref = engine.run(variant, params, W, S, want_hist=True)
+    got = wide.run_wide_local(variant, params, W, S, 3, want_hist=True)
+    torch.cuda.synchronize()
+    _compare(got, ref, wide.column_ranges(Mw, 3))

@@ -6,7 +6,7 @@ the product file carries no build switches.
 
 Patch sets live in tools/ab_patches.py: PATCHES[NAME] = [(old, new), ...];
 every `old` must occur exactly once in yuma_engine.hip (or give a third
-element, the expected count). "base" builds the unpatched source. Time the
+element, the expected count). "base" builds the unpatched source, "rev_<git rev>" that revision's source. Time the
 libraries with tools/ab_lib.sh or tools/phase_times.py (YUMA_HIP_LIB=...).
 Timing-only patches (results wrong by design) are named diag_*; they are
 never run by the tests."""
@@ -22,6 +22,10 @@ from ab_patches import PATCHES  # noqa: E402
 
 
 def patched(name: str) -> str:
+    if name.startswith("rev_"):  # the product source of a git revision, unpatched
+        rel = os.path.relpath(g.SRC, ROOT)
+        return subprocess.run(["git", "-C", ROOT, "show", f"{name[4:]}:{rel}"], check=True,
+                              capture_output=True, text=True).stdout
     s = open(g.SRC).read()
     for rep in PATCHES.get(name, []):
         old, new = rep[0], rep[1]
@@ -34,7 +38,7 @@ def patched(name: str) -> str:
 
 
 def build(name: str) -> str:
-    if name != "base" and name not in PATCHES:
+    if name != "base" and not name.startswith("rev_") and name not in PATCHES:
         raise SystemExit(f"unknown patch set {name}")
     os.makedirs(os.path.join(ROOT, "ablib"), exist_ok=True)
     src = os.path.join(os.path.dirname(g.SRC), f".ab_{name}.hip")  # next to the original: same includes

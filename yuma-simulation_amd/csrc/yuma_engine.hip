@@ -40,6 +40,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <type_traits>
 #include <vector>
 
 #include "yuma_hip.h"
@@ -127,6 +128,16 @@ __device__ __forceinline__ float div_rn(float a, const RowDiv& rd) {
   const float q = div_fast(a, rd, slow);
   return slow ? a / rd.d : q;
 }
+
+// Block barrier for an LDS hand-off only: waits for this wave's LDS traffic,
+// not for its global loads (__syncthreads()' workgroup fence would wait for
+// vmcnt(0), i.e. drain the loads in flight at every barrier).
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// a quantised consensus level as C (yumas.py:211 `.int() / 65_535`)
+__device__ __forceinline__ float level_value(int q) { return (float)q / 65535.0f; }
 
 // Input slice of a slice (epoch t, scenario n) = t N + n: the slice itself,
 // or epoch t when every scenario reads the same input trajectory (wsh: a
@@ -347,12 +358,25 @@ __device__ __forceinline__ void load4_vec(const float* __restrict__ v, int m, in
 // and added in chunk order by one lane — the same bits, and 4x the blocks
 // (one long wave per row leaves the last of ~3 dispatch rounds mostly idle).
 constexpr int kWideChunks = 64, kMaxWideChunks = 4096;
+// RN(1 / rs) when div_fast of every weight of the row by rs takes its fast
+// path (|rs| and every nonzero |w| in [2^-60, 2^60]; bmax / bmin1: the row's
+// max |w| and min nonzero |w| - 1 as bit patterns), else NaN: the sweep scan
+// then divides without a per-element guard (k_bonds_grp). k_rowsum stores it
+// per INPUT slice and row as rq4 = {row sum, this, normalised stake, 0}: one
+// 16-byte load per row and epoch.
+__device__ __forceinline__ float fast_row_rcp(float rs, unsigned bmax, unsigned bmin1) {
+  const float ad = fabsf(rs);
+  const bool ok = ad >= 0x1p-60f && ad <= 0x1p60f && bmax <= __float_as_uint(0x1p60f) &&
+                  (bmin1 == 0xFFFFFFFFu || bmin1 + 1u >= __float_as_uint(0x1p-60f));
+  return ok ? 1.0f / rs : qnan();
+}
 template <bool VEC, bool WIDE = false>
 __global__ __launch_bounds__(256) void k_rowsum(const float* __restrict__ W,
                                                 const float* __restrict__ S, int V, int M,
                                                 long long islice0, int rowblocks,
                                                 float* __restrict__ rsd, float* __restrict__ sn,
-                                                int partial, int* __restrict__ sx, int fan) {
+                                                int partial, int* __restrict__ sx, int fan,
+                                                float4* __restrict__ rq4) {
   // Block = 4 rows (WIDE: one row) of input slice wsl. Its row sums and
   // normalised stakes belong to output slices wsl·fan .. wsl·fan + fan - 1:
   // fan = 1, or N with shared inputs (they do not depend on the scenario:
@@ -360,8 +384,20 @@ __global__ __launch_bounds__(256) void k_rowsum(const float* __restrict__ W,
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const long long wsl = islice0 + blockIdx.x / rowblocks;
   const int rb = blockIdx.x % rowblocks;
+  // the fast-division screen of the row (rq4): max |w| and min nonzero |w|
+  // as bit patterns (|w| = 0 wraps to the maximum of bmin1)
+  unsigned bmax = 0u, bmin1 = 0xFFFFFFFFu;
+  auto screen = [&](const float (&x)[4]) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const unsigned b = __float_as_uint(x[c]) & 0x7FFFFFFFu;
+      bmax = b > bmax ? b : bmax;
+      bmin1 = b - 1u < bmin1 ? b - 1u : bmin1;
+    }
+  };
   if constexpr (WIDE) {
     __shared__ float qs[kMaxWideChunks];
+    __shared__ unsigned qb[2][4];
     const int nc = (M + 255) / 256;
     const float* r = W + (wsl * V + rb) * (long long)M;
 #pragma unroll 4
@@ -384,6 +420,15 @@ __global__ __launch_bounds__(256) void k_rowsum(const float* __restrict__ W,
       }
       const float q = wave_sum(((x[0] + x[1]) + x[2]) + x[3]);
       if (lane == 0) qs[k] = q;
+      screen(x);
+    }
+    for (int o = 1; o < 64; o <<= 1) {
+      bmax = max(bmax, (unsigned)__shfl_xor((int)bmax, o, 64));
+      bmin1 = min(bmin1, (unsigned)__shfl_xor((int)bmin1, o, 64));
+    }
+    if (lane == 0) {
+      qb[0][wave] = bmax;
+      qb[1][wave] = bmin1;
     }
     __syncthreads();
     if (wave == 0) {
@@ -393,6 +438,14 @@ __global__ __launch_bounds__(256) void k_rowsum(const float* __restrict__ W,
       acc = __shfl(acc, 0, 64);
       const float rs = partial ? acc : acc + 1e-6f;
       for (int f = lane; f < fan; f += 64) rsd[(wsl * fan + f) * V + rb] = rs;
+      if (rq4 != nullptr && lane == 0) {
+        unsigned bx = qb[0][0], bn = qb[1][0];
+        for (int w = 1; w < 4; ++w) {
+          bx = max(bx, qb[0][w]);
+          bn = min(bn, qb[1][w]);
+        }
+        *reinterpret_cast<float2*>(&rq4[wsl * V + rb]) = make_float2(rs, fast_row_rcp(rs, bx, bn));
+      }
     }
   }
   const int row = rb * 4 + wave;
@@ -420,10 +473,19 @@ __global__ __launch_bounds__(256) void k_rowsum(const float* __restrict__ W,
       float q = ((x[0] + x[1]) + x[2]) + x[3];
       q = wave_sum(q);  // the balanced tree over the chunk's 64 quads
       acc = acc + q;
+      screen(x);
     }
     // partial (column shard): the caller sums the shards, then k_add_eps
     const float rs = partial ? acc : acc + 1e-6f;
     for (int f = lane; f < fan; f += 64) rsd[(wsl * fan + f) * V + row] = rs;
+    if (rq4 != nullptr) {
+      for (int o = 1; o < 64; o <<= 1) {
+        bmax = max(bmax, (unsigned)__shfl_xor((int)bmax, o, 64));
+        bmin1 = min(bmin1, (unsigned)__shfl_xor((int)bmin1, o, 64));
+      }
+      if (lane == 0)
+        *reinterpret_cast<float2*>(&rq4[wsl * V + row]) = make_float2(rs, fast_row_rcp(rs, bmax, bmin1));
+    }
   }
   // the stake normalisation: output slices f = rb, rb + rowblocks, ... of
   // the fan (block 0 alone when fan = 1)
@@ -440,6 +502,7 @@ __global__ __launch_bounds__(256) void k_rowsum(const float* __restrict__ W,
     for (int v = lane; v < V; v += 64) {
       const float q = s[v] / acc;
       for (int f = rb; f < fan; f += rowblocks) sn[(wsl * fan + f) * V + v] = q;
+      if (rq4 != nullptr && rb == 0) reinterpret_cast<float*>(&rq4[wsl * V + v])[2] = q;
       const float f = q * 16777216.0f;
       exact &= f >= 0.0f && f <= 16777216.0f && __builtin_amdgcn_fractf(f) == 0.0f;
       units += exact ? (int)f : 0;
@@ -1203,6 +1266,261 @@ __global__ __launch_bounds__(256, 4) void k_consensus_w(const float* __restrict_
       if (m + c < M) craw[slice * M + m + c] = (double)hi_k[c] / (double)top;
 }
 
+// ---------------------------------------------------------------------------
+// Consensus, quantisation and rank from ONE read of W (run outputs: no
+// materialised Wn / Wc / T_v, no shared-input consensus classes, not Yuma2,
+// whose rank clips W_prev; yumas.py:192-217, YumaRust :78-106).
+// The rank needs the quantised consensus, i.e. ΣC over EVERY tile of the
+// slice (yumas.py:211), so it cannot run in the tile's consensus block
+// without a per-slice hand-off. k_cons_rank is a persistent grid (G blocks,
+// as many as fit at once, G a multiple of the tiles per slice) walking the
+// (slice, tile) items in slice-major order: block b takes items b, b + G,
+// b + 2G, ..., so a slice's tiles are one round of 64 consecutive blocks.
+// Per item the block runs k_consensus_w's load / normalisation / prerank /
+// search with the tile resident in registers and publishes the tile's C_raw
+// sum (an agent-scope counter per slice; the slice's last tile adds the tile
+// sums in order: csum_canonical's ΣC). One round later — while its next
+// item's W is in flight — it quantises its previous tile's columns with that
+// ΣC (k_quantise's formula) and ranks them from the tile still in registers
+// (two register sets, alternating), in k_rank_s's summation order. So the
+// slice's other blocks have a full round to publish; W is read once for
+// consensus and rank. Every wait only looks at items of the previous round
+// (all resident), and a bounded spin sets *err instead of hanging.
+// Liquid alpha (quantiles of all levels) runs after it in k_liquid.
+// ---------------------------------------------------------------------------
+struct ConsRankArgs {
+  const float* W;
+  const float* rsd;
+  const float* sn;
+  const int* sx;
+  const yuma_params_t* prm;
+  float* P;        // prerank (optional)
+  float* C;        // quantised consensus [slice][M]
+  int* qlev;       // its integer levels
+  float* R;        // rank
+  float* rpart;    // rank tile sums [slice][tile]
+  double* ctile;   // C_raw tile sums [slice - slice0][tile] (fp32 values, YumaRust fp64)
+  int* cnt;        // per slice: tiles published, +1 once ΣC is stored (zeroed before the launch)
+  float* sumc_f;   // ΣC per slice (chunk-relative, as k_liquid reads it)
+  double* sumc_d;
+  int* err;        // a wait ran out (never expected: every block is resident)
+  long long slice0, nslices;
+  int N, V, M, tiles;
+};
+
+constexpr int kConsRankSpin = 1 << 22;
+
+template <bool RUST>
+__global__ __launch_bounds__(256, 2) void k_cons_rank(ConsRankArgs A) {
+  constexpr int R = 16, NR = 16 * R, PL = NR / 64;
+  typedef typename std::conditional<RUST, double, float>::type T;
+  __shared__ __attribute__((aligned(16))) unsigned hb[kHistWords];
+  __shared__ __attribute__((aligned(16))) float rl[4][48 * R];
+  __shared__ T tred[2][4];      // C_raw wave sums of the item being published
+  __shared__ float rred[2][4];  // rank wave sums of the item being ranked
+  const WLay L = wlay();
+  const int V = A.V, M = A.M, tiles = A.tiles, N = A.N;
+  const long long items = A.nslices * tiles;
+  const long long G = gridDim.x;
+  const long long VM = (long long)V * M;
+
+  // the resident tile: normalised weights and the consensus grid index of
+  // this lane's 4 columns; the rows' sums / stakes / reciprocals in rl
+  float X[R][4];
+  int hX[4];
+  int par = 0;
+  for (long long it = blockIdx.x;; it += G, par ^= 1) {
+    const bool cur = it < items;  // block-uniform
+    const long long prv = it - G;
+    // --- rank of the previous round's item (its tile still in X, stakes in rl)
+    if (prv >= 0 && prv < items) {
+      const long long ps = A.slice0 + prv / tiles, pr = prv / tiles;
+      const int pt = (int)(prv % tiles);
+      const int pm = pt * kTileM + L.wave * 16 + L.cq * 4;
+      const int pn = (int)(ps % N);
+      const int iters = A.prm[pn].bisect_iters;
+      if (__hip_atomic_load(A.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+        for (int spin = 0; __hip_atomic_load(A.cnt + pr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) <= tiles;) {
+          __builtin_amdgcn_s_sleep(1);
+          if (++spin > kConsRankSpin) {  // never expected; later waits are skipped
+            __hip_atomic_store(A.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+          }
+        }
+      }
+      float Cq[4];
+      int lev[4];
+      const double top = (double)(1 << iters);
+      if constexpr (RUST) {
+        const double sd = __hip_atomic_load(A.sumc_d + pr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) lev[c] = (int)((double)hX[c] / top / sd * 65535.0);
+      } else {
+        const float sf = __hip_atomic_load(A.sumc_f + pr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) lev[c] = (int)((float)((double)hX[c] / top) / sf * 65535.0f);
+      }
+#pragma unroll
+      for (int c = 0; c < 4; ++c) Cq[c] = level_value(lev[c]);
+      const LdsRows s{&rl[0][0], L.wave * 48 * R + 16 * R + L.rg};
+      float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        const float si = s[i];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[c] = acc[c] + si * vmin(X[i][c], Cq[c]);
+      }
+#pragma unroll
+      for (int c = 0; c < 4; ++c) acc[c] = wsum16(acc[c]);
+      if (L.rg == 0)
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          if (pm + c < M) {
+            A.C[ps * M + pm + c] = Cq[c];
+            A.qlev[ps * M + pm + c] = lev[c];
+            A.R[ps * M + pm + c] = acc[c];
+          }
+      // the tile sum as the 64-lane butterfly over the tile's miners
+      float q = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+      q = q + __shfl_xor(q, 16, 64);
+      q = q + __shfl_xor(q, 32, 64);
+      if (L.lane == 0) rred[par][L.wave] = q;
+      lds_barrier();
+      if (threadIdx.x == 0)
+        A.rpart[ps * tiles + pt] = (rred[par][0] + rred[par][1]) + (rred[par][2] + rred[par][3]);
+    }
+    if (!cur) break;
+    long long slice = 0;
+    int tile = 0, m = 0;
+    float dv[PL], sv[PL];
+    bool full = true, allfull = true;
+    {
+      slice = A.slice0 + it / tiles;
+      tile = (int)(it % tiles);
+      m = tile * kTileM + L.wave * 16 + L.cq * 4;
+      const float* Ws = A.W + slice * VM;
+      const float* rsd_s = A.rsd + slice * V;
+      const float* sn_s = A.sn + slice * V;
+#pragma unroll
+      for (int k = 0; k < PL; ++k) {
+        const int jj = min(L.lane + 64 * k, V - 1);
+        dv[k] = rsd_s[jj];
+        sv[k] = sn_s[jj];
+      }
+      full = L.rg + 16 * (R - 1) < V && m + 3 < M;
+      allfull = __all(full);
+      if (allfull) {
+        unsigned o0 = (unsigned)L.rg * (unsigned)M + (unsigned)m, st = 16u * (unsigned)M;
+        // opaque per item: the compiler would otherwise hoist the 16 row
+        // offsets out of the persistent loop (16 more live registers)
+        asm volatile("" : "+v"(o0), "+s"(st));
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+          const float4 t = *reinterpret_cast<const float4*>(Ws + (o0 + (unsigned)i * st));
+          X[i][0] = t.x;
+          X[i][1] = t.y;
+          X[i][2] = t.z;
+          X[i][3] = t.w;
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < R; ++i) load4c<true>(Ws, L.rg + 16 * i, V, m, M, X[i]);
+      }
+    }
+    // --- consensus of this round's item (k_consensus_w on a resident tile)
+    {
+      float* rlw = &rl[L.wave][0];
+      float amax = 0.0f, dmin = INFINITY;
+#pragma unroll
+      for (int k = 0; k < PL; ++k) {
+        const int j = L.lane + 64 * k;
+        amax = fmaxf(amax, fabsf(dv[k]));
+        dmin = fminf(dmin, fabsf(dv[k]));
+        rlw[j] = dv[k];
+        rlw[NR + j] = j < V ? sv[k] : 0.0f;
+        rlw[2 * NR + j] = 1.0f / dv[k];
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      typedef float f2 __attribute__((ext_vector_type(2)));
+      unsigned ymin = 0xFFFFFFFFu;
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        const float d = rlw[L.rg + 16 * i];
+        const float r = rlw[2 * NR + L.rg + 16 * i];
+        const f2 r2 = {r, r}, nd2 = {-d, -d};
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const f2 a2 = {X[i][2 * h], X[i][2 * h + 1]};
+#pragma unroll
+          for (int c = 0; c < 2; ++c) {
+            amax = fmaxf(amax, fabsf(a2[c]));
+            const unsigned y = (__float_as_uint(a2[c]) << 1) - 1u;
+            ymin = y < ymin ? y : ymin;
+          }
+          const f2 q = a2 * r2;
+          const f2 e = __builtin_elementwise_fma(nd2, q, a2);
+          const f2 q1 = __builtin_elementwise_fma(e, r2, q);
+          X[i][2 * h] = q1[0];
+          X[i][2 * h + 1] = q1[1];
+        }
+      }
+      const bool slow = !(dmin >= 0x1p-60f && amax <= 0x1p60f &&
+                          (ymin == 0xFFFFFFFFu || ymin + 1u >= (__float_as_uint(0x1p-60f) << 1)));
+      if (__any(slow)) {  // rare: some operand outside the fast-division guard
+        const float* Ws = A.W + slice * VM;
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+          load4c<true>(Ws, L.rg + 16 * i, V, m, M, X[i]);
+          const float d = rlw[L.rg + 16 * i];
+#pragma unroll
+          for (int c = 0; c < 4; ++c) X[i][c] = X[i][c] / d;
+        }
+      }
+      if (!allfull) {
+#pragma unroll
+        for (int i = 0; i < R; ++i) mask4(L.rg + 16 * i, V, m, M, X[i]);
+      }
+    }
+    const LdsRows s{&rl[0][0], L.wave * 48 * R + 16 * R + L.rg};
+    const int n = (int)(slice % N);
+    if (A.P != nullptr) prerank_store<R>(X, s, L, m, M, A.P + slice * M);
+    const yuma_params_t& p = A.prm[n];
+    const bool hist_ok = !(p.flags & YUMA_FLAG_NO_HIST);
+    consensus_search<R, 16>(X, s, p.kappa, p.bisect_iters, hist_ok ? A.sx[slice] : -1,
+                            hb + L.wave * 16 * kHS, L.lane, L.cq, L.rg, hX);
+    // --- publish the tile's C_raw sum (csum_canonical's in-tile butterfly)
+    {
+      const double top = (double)(1 << p.bisect_iters);
+      T v[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) v[c] = m + c < M ? (T)((double)hX[c] / top) : (T)0;
+      T q = (v[0] + v[1]) + (v[2] + v[3]);
+      q = q + __shfl_xor(q, 16, 64);
+      q = q + __shfl_xor(q, 32, 64);
+      if (L.lane == 0) tred[par][L.wave] = q;
+      lds_barrier();
+      if (threadIdx.x == 0) {
+        const long long sr = slice - A.slice0;
+        const T ts = (tred[par][0] + tred[par][1]) + (tred[par][2] + tred[par][3]);
+        __hip_atomic_store(A.ctile + sr * tiles + tile, (double)ts, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int old = __hip_atomic_fetch_add(A.cnt + sr, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        if (old == tiles - 1) {  // the slice's last tile: ΣC, tiles in order
+          T tot = (T)0;
+          for (int k = 0; k < tiles; ++k)
+            tot = tot + (T)__hip_atomic_load(A.ctile + sr * tiles + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if constexpr (RUST)
+            __hip_atomic_store(A.sumc_d + sr, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          else
+            __hip_atomic_store(A.sumc_f + sr, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_fetch_add(A.cnt + sr, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+    }
+  }
+}
+
 // Clip + rank (yumas.py:214-217; Yuma2 clips W_prev :328), wave-owned columns.
 // rpart[slice][tile] = sum over the tile's 64 miners (wave sums, waves in order).
 template <int R, bool VEC, bool YUMA2, bool FULL>
@@ -1319,14 +1637,20 @@ __global__ __launch_bounds__(256) void k_rank_w(
   }
 }
 
-// Clip + rank, streaming form for run outputs (no Wn / Wc / T_v, not Yuma2):
+// Clip + rank, streaming form for run outputs (no Wn / Wc / T_v):
 // R[m] = sum_v S[v] min(W[v,m], C[m]) (yumas.py:439-442). Nothing is held
 // across rows, so the block takes the bond kernel's wide layout (a wave
 // instruction moves 4 rows x 256 contiguous bytes instead of 16 x 64) and
 // streams its rows in batches of 8 loads per lane. Order: rows g, g+16, ...
-// sequentially per lane, then the 4 row groups of a wave (xor 16, 32), then
-// the 4 waves in order.
-template <bool VEC>
+// sequentially per lane, then the 16 row groups as a pairwise tree (the 4 row
+// groups of a wave by xor 16, 32; the 4 waves as (w0 + w1) + (w2 + w3)) —
+// the order of the DPP row tree wsum16 over rows rg + 16 i, so k_cons_rank
+// (rank from the consensus kernel's resident tile) gives the same bits. The
+// tile sum is the 64-lane butterfly over the tile's miners. YUMA2 clips the previous epoch's normalised weights
+// instead (yumas.py:299-300, 328-331: W_prev, at the first epoch the caller's
+// W_prev or W itself) with this epoch's stakes: the previous slice divided by
+// its own row sums — only W_prev is read, not W.
+template <bool VEC, bool YUMA2 = false>
 __global__ __launch_bounds__(256, 1) void k_rank_s(const float* __restrict__ W,
                                                 const float* __restrict__ rsd,
                                                 const float* __restrict__ sn,
@@ -1334,7 +1658,8 @@ __global__ __launch_bounds__(256, 1) void k_rank_s(const float* __restrict__ W,
                                                 long long slice0, int tiles,
                                                 float* __restrict__ Rout,
                                                 float* __restrict__ rpart, int wsh,
-                                                const int* __restrict__ crep) {
+                                                const int* __restrict__ crep,
+                                                const float* __restrict__ Wprev_init) {
   __shared__ float4 red[4][16];
   const Lay L = lay();
   const long long slice = slice0 + blockIdx.x / tiles;
@@ -1342,7 +1667,19 @@ __global__ __launch_bounds__(256, 1) void k_rank_s(const float* __restrict__ W,
   if (dup_slice(crep, slice, N)) return;  // block-uniform
   const long long VM = (long long)V * M;
   const int m = tile * kTileM + L.c4 * 4;
+  // the clipped matrix and the row sums that normalise it (block-uniform)
+  long long wsl = slice;
+  bool divide = true;
   const float* Ws = W + in_slice(slice, N, wsh) * VM;
+  if (YUMA2) {
+    if (slice >= N) {
+      wsl = slice - N;
+      Ws = W + in_slice(wsl, N, wsh) * VM;
+    } else if (Wprev_init != nullptr) {
+      Ws = Wprev_init + (slice % N) * VM;  // already normalised
+      divide = false;
+    }
+  }
   float Cc[4];
   load4c<VEC>(C + slice * M, 0, 1, m, M, Cc);
   float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
@@ -1353,24 +1690,26 @@ __global__ __launch_bounds__(256, 1) void k_rank_s(const float* __restrict__ W,
     for (int i = 0; i < B; ++i) {
       const int rr = min(r0 + 16 * i, V - 1);
       load4c<VEC>(Ws, rr, V, m, M, w[i]);
-      d[i] = rsd[slice * V + rr];
+      d[i] = rsd[wsl * V + rr];
       s[i] = sn[slice * V + rr];
     }
-    bool slow = false;
-#pragma unroll
-    for (int i = 0; i < B; ++i) {
-      const RowDiv rdv = row_div(d[i]);
-#pragma unroll
-      for (int c = 0; c < 4; ++c) w[i][c] = div_fast_nz(w[i][c], rdv, slow);
-    }
-    if (__any(slow)) {  // rare: redo the batch with IEEE division (wave-uniform)
+    if (!YUMA2 || divide) {
+      bool slow = false;
 #pragma unroll
       for (int i = 0; i < B; ++i) {
-        const int rr = min(r0 + 16 * i, V - 1);
-        float x[4];
-        load4c<VEC>(Ws, rr, V, m, M, x);
+        const RowDiv rdv = row_div(d[i]);
 #pragma unroll
-        for (int c = 0; c < 4; ++c) w[i][c] = x[c] / d[i];
+        for (int c = 0; c < 4; ++c) w[i][c] = div_fast_nz(w[i][c], rdv, slow);
+      }
+      if (__any(slow)) {  // rare: redo the batch with IEEE division (wave-uniform)
+#pragma unroll
+        for (int i = 0; i < B; ++i) {
+          const int rr = min(r0 + 16 * i, V - 1);
+          float x[4];
+          load4c<VEC>(Ws, rr, V, m, M, x);
+#pragma unroll
+          for (int c = 0; c < 4; ++c) w[i][c] = x[c] / d[i];
+        }
       }
     }
 #pragma unroll
@@ -1390,9 +1729,7 @@ __global__ __launch_bounds__(256, 1) void k_rank_s(const float* __restrict__ W,
   if (L.wave == 0) {
     // lane l: miner tile*64 + l
     const float* rf = reinterpret_cast<const float*>(&red[0][0]);
-    float r = rf[L.lane];
-#pragma unroll
-    for (int w = 1; w < 4; ++w) r = r + rf[w * 64 + L.lane];
+    const float r = (rf[L.lane] + rf[64 + L.lane]) + (rf[128 + L.lane] + rf[192 + L.lane]);
     const int mg = tile * kTileM + L.lane;
     if (mg < M) Rout[slice * M + mg] = r;
     float t = mg < M ? r : 0.0f;
@@ -1426,6 +1763,40 @@ __device__ double block_sum_d(double x, double* red) {
   double t = red[0];
   for (int w = 1; w < NW; ++w) t = t + red[w];
   return t;
+}
+
+// ΣC_raw in the engine's canonical order (yumas.py:211 `C.sum()`, YumaRust
+// :97 in fp64): each 64-miner tile summed as the 64-lane butterfly over its
+// columns (padding 0), the tile sums added in tile order. k_quantise, k_csum
+// (per shard, then the shards in order) and k_cons_rank (each block its tile;
+// the last block of a slice adds the tiles) give the same bits. T = float
+// (the fp32 sum of (float) C_raw) or double (YumaRust).
+constexpr int kCsumStage = 1024;
+template <typename T, int NT>
+__device__ T csum_canonical(const double* __restrict__ cr, int M, T* stage /*[kCsumStage + 1]*/) {
+  constexpr int NW = NT / 64;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int tiles = (M + 63) / 64;
+  T acc = (T)0;
+  for (int k0 = 0; k0 < tiles; k0 += kCsumStage) {
+    const int nk = min(tiles - k0, kCsumStage);
+    for (int k = wave; k < nk; k += NW) {
+      const int m = (k0 + k) * 64 + lane;
+      T v = m < M ? (T)cr[m] : (T)0;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) v = v + __shfl_xor(v, o, 64);
+      if (lane == 0) stage[k] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0)
+      for (int k = 0; k < nk; ++k) acc = acc + stage[k];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) stage[kCsumStage] = acc;
+  __syncthreads();
+  const T tot = stage[kCsumStage];
+  __syncthreads();
+  return tot;
 }
 
 // high-byte histogram of the levels (four loads in flight per thread)
@@ -1490,7 +1861,6 @@ __device__ int select_level(const int* __restrict__ q, int M, int k, const int* 
   return r;
 }
 
-__device__ __forceinline__ float level_value(int q) { return (float)q / 65535.0f; }
 
 // torch.quantile(C, qf) on levels (Sorting.cpp: rank = q*(n-1) in fp32,
 // weight = rank - floor, lerp in the FMA form of the vectorised lerp kernel).
@@ -1524,8 +1894,7 @@ __global__ __launch_bounds__(NT) void k_quantise(const double* __restrict__ craw
                                                  const float* __restrict__ ext_sumf,
                                                  const double* __restrict__ ext_sumd,
                                                  int no_liquid, const int* __restrict__ crep) {
-  __shared__ float redf[NT / 64];
-  __shared__ double redd[NT / 64];
+  __shared__ double stage[kCsumStage + 1];
   __shared__ int hist1[256], hist2[256], bc[4];
   const long long slice = slice0 + blockIdx.x;
   const yuma_params_t& p = prm[slice % N];
@@ -1544,30 +1913,10 @@ __global__ __launch_bounds__(NT) void k_quantise(const double* __restrict__ craw
       sumf = ext_sumf[slice];
     }
   } else if (variant == YUMA_VARIANT_RUST) {
-    double acc = 0.0;
-    int m = threadIdx.x;
-    for (; m + 3 * NT < M; m += 4 * NT) {  // loads in flight, same summation order
-      const double x0 = cr[m], x1 = cr[m + NT], x2 = cr[m + 2 * NT], x3 = cr[m + 3 * NT];
-      acc = acc + x0;
-      acc = acc + x1;
-      acc = acc + x2;
-      acc = acc + x3;
-    }
-    for (; m < M; m += NT) acc = acc + cr[m];
-    sumd = block_sum_d<NT>(acc, redd);
+    sumd = csum_canonical<double, NT>(cr, M, stage);
     sumf = (float)sumd;
   } else {
-    float acc = 0.0f;
-    int m = threadIdx.x;
-    for (; m + 3 * NT < M; m += 4 * NT) {  // loads in flight, same summation order
-      const double x0 = cr[m], x1 = cr[m + NT], x2 = cr[m + 2 * NT], x3 = cr[m + 3 * NT];
-      acc = acc + (float)x0;
-      acc = acc + (float)x1;
-      acc = acc + (float)x2;
-      acc = acc + (float)x3;
-    }
-    for (; m < M; m += NT) acc = acc + (float)cr[m];
-    sumf = block_sum<NT>(acc, redf);
+    sumf = csum_canonical<float, NT>(cr, M, reinterpret_cast<float*>(stage));
   }
   for (int m = threadIdx.x; m < M; m += NT) {
     int lev;
@@ -1858,6 +2207,7 @@ struct BondArgs {
   float* Wb_out;
   float* Binst_out;
   float* dpart;
+  const float4* rq4;  // per input slice and row {row sum, RN(1 / row sum) or NaN, stake, 0} (k_rowsum)
   int N, V, M, tiles, rowblocks, t0, t1;
   int wsh;      // every scenario reads input slice t (yuma_run_shared)
   int cblocks;  // k_bonds_elem: column blocks of CB miners per row block
@@ -2139,6 +2489,286 @@ __global__ __launch_bounds__(NT) void k_bonds(BondArgs A) {
 }
 
 // ---------------------------------------------------------------------------
+// Phase 2, column-normalised variants for run outputs (YumaRust yumas.py:
+// 113-116 + 142-149, Yuma :227-258, Yuma2 :341-372): the bond matrix is
+// normalised over every validator of a miner column each epoch, so a block
+// owns whole columns — all V rows of a 16-miner strip (one block per strip
+// and scenario: 256 blocks at 4096 miners, where k_bonds' 64-miner columns
+// give 64) — and walks the epochs with the strip's bond state in registers
+// and the inputs of the next P epochs in flight, like k_bonds_elem.
+// Layout: 512 threads; lane (cq, rr) = (lane >> 4, lane & 15) of wave w owns
+// miners 4 cq .. 4 cq + 3 of rows rr + 16 w + 128 i (i < R), so the 16 rows of
+// a column quad are one DPP row. Column sums (Σ_v S·W_b, and YumaRust's
+// Σ_v B_ema): per-thread rows in order, the DPP row tree (wsum16), then the
+// 8 waves in order through LDS; every lane ends with the same bits. The LDS
+// hand-off waits for LDS traffic only (lds_barrier), so the epoch prefetch
+// ring stays in flight across it. Dividend partials per (row, 16-miner
+// strip): [slice][strip][V], k_finalize adds the strips.
+// ---------------------------------------------------------------------------
+constexpr int kCnStrip = 16;  // miners per column-normalised block
+
+
+// Sum over the 8 waves (in order) of per-wave column partials: wave w's DPP
+// row tree result for the 16 strip columns sits in red[w][0..15].
+__device__ __forceinline__ void cn_wave_sums(float (&x)[4], float (*red)[kCnStrip], int cq, int rr,
+                                             int wave) {
+#pragma unroll
+  for (int c = 0; c < 4; ++c) x[c] = wsum16(x[c]);
+  if (rr == 0) *reinterpret_cast<float4*>(&red[wave][cq * 4]) = make_float4(x[0], x[1], x[2], x[3]);
+  lds_barrier();
+  float4 a = *reinterpret_cast<const float4*>(&red[0][cq * 4]);
+#pragma unroll
+  for (int w = 1; w < 8; ++w) {
+    const float4 b = *reinterpret_cast<const float4*>(&red[w][cq * 4]);
+    a.x = a.x + b.x;
+    a.y = a.y + b.y;
+    a.z = a.z + b.z;
+    a.w = a.w + b.w;
+  }
+  x[0] = a.x;
+  x[1] = a.y;
+  x[2] = a.z;
+  x[3] = a.w;
+}
+
+template <int VARIANT, int R, int P>
+__global__ __launch_bounds__(512, 1) void k_bonds_cn(BondArgs A) {
+  constexpr bool RUST = VARIANT == YUMA_VARIANT_RUST, YUMA2 = VARIANT == YUMA_VARIANT_YUMA2;
+  __shared__ __attribute__((aligned(16))) float red[2][8][kCnStrip];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int cq = lane >> 4, rr = lane & 15;
+  const int strip = blockIdx.x % A.cblocks;
+  const int n = blockIdx.x / A.cblocks;
+  const int N = A.N, V = A.V, M = A.M;
+  const long long VM = (long long)V * M;
+  const int m = strip * kCnStrip + cq * 4;
+  const bool colok = m < M;  // M % 4 == 0: a column quad is wholly in or out
+  const int mc = colok ? m : M - 4;
+  const int row0 = rr + 16 * wave;
+  // every parameter read once into registers (a load inside the epoch loop
+  // would wait on the prefetch ring)
+  const yuma_params_t& pg = A.prm[n];
+  const bool liquid = pg.liquid_mode != YUMA_LIQUID_OFF;
+  const float p_ba = pg.bond_alpha, p_omba = pg.one_minus_bond_alpha;
+  const float p_pen = pg.bond_penalty, p_ompen = pg.one_minus_bond_penalty;
+
+  float B[R][4];
+  bool has_old;
+  {
+    const float* src = A.t0 == 0 ? A.B_init : A.Bstate;
+    has_old = src != nullptr;
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const int row = row0 + 128 * i;
+      if (has_old && row < V && colok)
+        load4<true>(src + n * VM + (long long)row * M, m, M, B[i]);
+      else
+#pragma unroll
+        for (int c = 0; c < 4; ++c) B[i][c] = 0.0f;
+    }
+  }
+  // Yuma2: the previous epoch's normalised weights (yumas.py:299-300, 328)
+  float Wp[R][4];
+  bool have_wp = false;
+  if constexpr (YUMA2) {
+#pragma unroll
+    for (int i = 0; i < R; ++i)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) Wp[i][c] = 0.0f;
+    if (A.t0 == 0) {
+      if (A.Wprev_init != nullptr) {
+        have_wp = true;
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+          const int row = row0 + 128 * i;
+          if (row < V && colok) load4<true>(A.Wprev_init + n * VM + (long long)row * M, m, M, Wp[i]);
+        }
+      }
+    } else {
+      have_wp = true;
+      const long long ps = (long long)(A.t0 - 1) * N + n;
+      const long long pw = A.wsh ? (long long)(A.t0 - 1) : ps;
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        const int row = row0 + 128 * i;
+        if (row < V && colok) {
+          float x[4];
+          load4<true>(A.W + pw * VM + (long long)row * M, m, M, x);
+          const float d = A.rsd[ps * V + row];
+#pragma unroll
+          for (int c = 0; c < 4; ++c) Wp[i][c] = x[c] / d;
+        }
+      }
+    }
+  }
+
+  // the inputs of the next P epochs in flight: W rows, row sums, stakes, and
+  // the strip's consensus, incentive and (liquid) bond_alpha
+  float rw[P][R][4], rd[P][R], rsn[P][R], rcc[P][4], ri[P][4], rba[P][4];
+  auto fetch = [&](int k, int t) {
+    const long long slice = (long long)t * N + n;
+    const float* Wt = A.W + (A.wsh ? (long long)t : slice) * VM;
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const int rr_ = min(row0 + 128 * i, V - 1);
+      const float4 x = *reinterpret_cast<const float4*>(Wt + (long long)rr_ * M + mc);
+      rw[k][i][0] = x.x;
+      rw[k][i][1] = x.y;
+      rw[k][i][2] = x.z;
+      rw[k][i][3] = x.w;
+      rd[k][i] = A.rsd[slice * V + rr_];
+      rsn[k][i] = A.sn[slice * V + rr_];
+    }
+    load4c<true>(A.C + slice * M, 0, 1, m, M, rcc[k]);
+    load4c<true>(A.I + slice * M, 0, 1, m, M, ri[k]);
+    if (liquid) load4c<true>(A.ba + slice * M, 0, 1, m, M, rba[k]);
+  };
+#pragma unroll
+  for (int k = 0; k < P; ++k)
+    if (A.t0 + k < A.t1) fetch(k, A.t0 + k);
+
+  int par = 0;  // LDS buffer of this epoch's first column sum
+  for (int tb = A.t0; tb < A.t1; tb += P) {
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+      const int t = tb + k;
+      if (t >= A.t1) break;
+      const long long slice = (long long)t * N + n;
+      float bac[4], omba[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        bac[c] = liquid ? rba[k][c] : p_ba;
+        omba[c] = liquid ? 1.0f - rba[k][c] : p_omba;
+      }
+      // normalised weights (yumas.py:186), padding rows / columns zero
+      float wn[R][4], s[R];
+      {
+        bool slow = false;
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+          const RowDiv rdv = row_div(rd[k][i]);
+#pragma unroll
+          for (int c = 0; c < 4; ++c) wn[i][c] = div_fast(rw[k][i][c], rdv, slow);
+        }
+        if (__any(slow)) {
+#pragma unroll
+          for (int i = 0; i < R; ++i)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) wn[i][c] = rw[k][i][c] / rd[k][i];
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        const bool live = row0 + 128 * i < V;
+        s[i] = live ? rsn[k][i] : 0.0f;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) wn[i][c] = (live && colok) ? wn[i][c] : 0.0f;
+      }
+      // instantaneous bonds: S·W_b (Yuma, Yuma2: W_b = (1-β) W + β Wc;
+      // YumaRust: S·Wc) over their column sums
+      float num[R][4], csum[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+      for (int i = 0; i < R; ++i)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const float src = (YUMA2 && have_wp) ? Wp[i][c] : wn[i][c];
+          const float wc = tmin(src, rcc[k][c]);
+          const float wb = RUST ? wc : p_ompen * src + p_pen * wc;
+          num[i][c] = s[i] * wb;
+          csum[c] = csum[c] + num[i][c];
+        }
+      if constexpr (YUMA2) {
+#pragma unroll
+        for (int i = 0; i < R; ++i)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) Wp[i][c] = wn[i][c];
+        have_wp = true;
+      }
+      float ic[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) ic[c] = ri[k][c];
+      if (t + P < A.t1) fetch(k, t + P);  // slot k consumed: refill it
+      cn_wave_sums(csum, red[par], cq, rr, wave);
+      par ^= 1;
+      float ema[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+      {
+        RowDiv cd[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) cd[c] = row_div(RUST ? csum[c] + 1e-6f : csum[c]);
+        float bi[R][4];
+        bool slow = false;
+#pragma unroll
+        for (int i = 0; i < R; ++i)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) bi[i][c] = div_fast(num[i][c], cd[c], slow);
+        if (__any(slow)) {
+#pragma unroll
+          for (int i = 0; i < R; ++i)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) bi[i][c] = num[i][c] / cd[c].d;
+        }
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+          const bool live = row0 + 128 * i < V;
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            const float b = nan_to_num(bi[i][c], 0.0f);
+            float e = has_old ? bac[c] * b + omba[c] * B[i][c] : b;
+            e = (live && colok) ? e : 0.0f;
+            B[i][c] = e;
+            ema[c] = ema[c] + e;
+          }
+        }
+      }
+      if constexpr (RUST) {  // B_ema / (Σ_v B_ema + 1e-6), nan_to_num (yumas.py:147-149)
+        cn_wave_sums(ema, red[par], cq, rr, wave);
+        par ^= 1;
+        RowDiv cd[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) cd[c] = row_div(ema[c] + 1e-6f);
+        float q[R][4];
+        bool slow = false;
+#pragma unroll
+        for (int i = 0; i < R; ++i)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) q[i][c] = div_fast(B[i][c], cd[c], slow);
+        if (__any(slow)) {
+#pragma unroll
+          for (int i = 0; i < R; ++i)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) q[i][c] = B[i][c] / cd[c].d;
+        }
+#pragma unroll
+        for (int i = 0; i < R; ++i)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) B[i][c] = nan_to_num(q[i][c], 0.0f);
+      }
+      has_old = true;
+      // bond history and the dividend partials Σ_{m in strip} B·I (the four
+      // column quads of a row: lanes l, l^16, l^32, l^48)
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        const int row = row0 + 128 * i;
+        if (A.B_hist != nullptr && row < V && colok)
+          __builtin_nontemporal_store(fvec4{B[i][0], B[i][1], B[i][2], B[i][3]},
+                                      reinterpret_cast<fvec4*>(A.B_hist + slice * VM + (long long)row * M + m));
+        float d = 0.0f;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) d = d + B[i][c] * ic[c];
+        d = colok ? d : 0.0f;
+        d = qsum4(d);
+        if (cq == 0 && row < V) A.dpart[(slice * A.cblocks + strip) * (long long)V + row] = d;
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    const int row = row0 + 128 * i;
+    if (row < V && colok) store4<true>(A.Bstate + n * VM + (long long)row * M, m, M, B[i]);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Phase 2, element-wise variants (Yuma3 yumas.py:452-472, Yuma4 :570-586):
 // a software-pipelined scan. Each thread owns R rows x 4 miners of the bond
 // tile in registers and keeps the inputs of the next P epochs in flight
@@ -2325,26 +2955,28 @@ __global__ __launch_bounds__(BS, 1) void k_bonds_elem(BondArgs A) {
 // Phase 2 for parameter sweeps over ONE input trajectory (shared inputs,
 // config c3), element-wise variants: a block runs the scan of K scenarios
 // side by side over one 16 R-row x 64-miner tile of W. Every scenario of the
-// sweep reads the same W[t]; k_bonds_elem's per-scenario blocks fetch W once
-// per scenario from beyond L2 (69.6 GB per c3 step: profiles/r03/c3). Here
-// W[t], the row sums and the normalised weights are loaded and divided once
-// per K scenarios; each scenario keeps its own bond tile in registers and its
-// own parameters, resets, liquid bond_alpha and dividend partials — the same
-// operations in the same order as k_bonds_elem, so the same bits. c3 bonds
-// 10.4 ms (K = 1) -> 9.9 (K = 2), 10.3 (K = 4), 15.1 (K = 8: 204 VGPRs and
-// SGPR spills), same box (profiles/r03/ab/c3_scan_groups.txt). The loop is
-// issue-bound, on the scalar side: per-lane pointers advanced by a stride
-// per epoch instead of 64-bit slice-index products took its SALU from 137 to
-// 38 per two epochs and its SGPR spills from 48 to 22 (9.9 -> 9.1 ms);
-// packed-pair f32 math (no gain: v_pk_* issue as two ops on gfx950) and an
-// XCD-grouped block order (9.4-9.5 ms) were tried and dropped. Fixed-alpha
-// scenarios keep bond_alpha in the liquid operand (no per-element selects)
-// under a 6-waves-per-SIMD bound: 9.1 -> 8.6 ms
-// (profiles/r03/ab/c3_grp_alpha_operands.txt).
+// sweep reads the same W[t]; W[t], the row sums and the normalised weights
+// are loaded and divided once per K scenarios; each scenario keeps its own
+// bond tile in registers and its own parameters, resets, liquid bond_alpha
+// and dividend partials — the same operations in the same order as
+// k_bonds_elem, so the same bits. The scan is bound by instruction issue,
+// not by HBM (W is re-read from the caches; profiles/r03/c3sq), so the
+// per-element work is cut to the bond update itself:
+//  * the row division takes k_rowsum's RN(1/row sum) (rq4), NaN when some
+//    weight or the row sum leaves the fast division's range: no per-row IEEE
+//    reciprocal and no per-element guard (a wave whose rows are not all in
+//    range divides in IEEE, same bits);
+//  * blocks whose scenarios all use a fixed bond_alpha (LIQ = false) take
+//    bond_alpha / 1 - bond_alpha as block-uniform operands; liquid (or mixed)
+//    blocks the per-miner operands with the exact one_minus_bond_alpha
+//    correction for their fixed-alpha scenarios (p_corr);
+// History (round 3): K = 2 beats 1 / 3 / 4 / 8 (profiles/r03/ab/
+// c3_scan_group_k.txt); packed-pair f32 math and an XCD-grouped block order
+// lost.
 // ---------------------------------------------------------------------------
 constexpr int kGrpWaves = 6;  // minimum waves per SIMD of the sweep scan
-template <int VARIANT, int K, int R, int P>
-__global__ __launch_bounds__(256, kGrpWaves) void k_bonds_grp(BondArgs A) {
+template <int VARIANT, int K, int R, int P, bool LIQ>
+__device__ __forceinline__ void grp_scan(const BondArgs& A, unsigned liquid_mask) {
   constexpr int G = 16;
   const Lay L = lay();
   const int tile = blockIdx.x % A.tiles;
@@ -2360,7 +2992,7 @@ __global__ __launch_bounds__(256, kGrpWaves) void k_bonds_grp(BondArgs A) {
   // would wait on the prefetches, see k_bonds_elem)
   float p_ba[K], p_omba[K], p_maxint[K], p_ca[K], p_dk[K];
   int p_rmode[K], p_repoch[K], p_rindex[K];
-  unsigned liquid_mask = 0, rall_mask = 0;
+  unsigned rall_mask = 0;
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     const yuma_params_t& pg = A.prm[min(n0 + k, N - 1)];
@@ -2372,7 +3004,6 @@ __global__ __launch_bounds__(256, kGrpWaves) void k_bonds_grp(BondArgs A) {
     p_rmode[k] = pg.reset_mode;
     p_repoch[k] = pg.reset_epoch;
     p_rindex[k] = pg.reset_index;
-    if (pg.liquid_mode != YUMA_LIQUID_OFF) liquid_mask |= 1u << k;
     if (pg.flags & YUMA_FLAG_RESET_ALL_COLUMNS) rall_mask |= 1u << k;
   }
 
@@ -2395,25 +3026,23 @@ __global__ __launch_bounds__(256, kGrpWaves) void k_bonds_grp(BondArgs A) {
   }
 
   // Addressing: per-lane pointers (load4c's clamped row and column folded
-  // in) that advance by a constant stride per epoch, instead of 64-bit
-  // slice-index products per epoch and scenario on the scalar unit: the loop
-  // was bound by scalar issue (137 SALU against 188 VALU per two epochs, and
-  // SGPR spills), not by the vector work (profiles/r03/c3sq).
+  // in) advanced by a constant stride per epoch (one v_lshl_add_u64 each);
+  // block-uniform bases instead keep ~12 64-bit pointers live in SGPRs and
+  // spill them (k_bonds_grp<4,2,1,2>: 148 SGPR spills, 507 v_readlane /
+  // v_writelane against 88).
   const int mc = m < M ? m : M - 4;
-  const long long sV = (long long)N * V, sM = (long long)N * M, sD = (long long)N * A.tiles * V;
+  const long long sM = (long long)N * M, sD = (long long)N * A.tiles * V;
 
-  // the shared inputs of the next P epochs in flight: W rows and the row
-  // sums / stakes (k_rowsum stored them for every scenario; scenario n0's)
-  float rw[P][R][4], rd[P][R], rsn[P][R];
+  // the shared inputs of the next P epochs in flight: W rows and their
+  // {row sum, reciprocal, stake} (k_rowsum's rq4, per input epoch)
+  float rw[P][R][4], rd[P][R], rq[P][R], rsn[P][R];
   const float* fW[R];  // next epoch to fetch
-  const float* fR[R];
-  const float* fS[R];
+  const float4* fQ[R];
 #pragma unroll
   for (int i = 0; i < R; ++i) {
     const int rr = min(row0 + G * i, V - 1);
     fW[i] = A.W + (long long)A.t0 * VM + (long long)rr * M + mc;
-    fR[i] = A.rsd + ((long long)A.t0 * N + n0) * V + rr;
-    fS[i] = A.sn + ((long long)A.t0 * N + n0) * V + rr;
+    fQ[i] = A.rq4 + (long long)A.t0 * V + rr;
   }
   auto fetch = [&](int kk, bool load) {
 #pragma unroll
@@ -2424,21 +3053,22 @@ __global__ __launch_bounds__(256, kGrpWaves) void k_bonds_grp(BondArgs A) {
         rw[kk][i][1] = x.y;
         rw[kk][i][2] = x.z;
         rw[kk][i][3] = x.w;
-        rd[kk][i] = *fR[i];
-        rsn[kk][i] = *fS[i];
+        const float4 q = *fQ[i];
+        rd[kk][i] = q.x;
+        rq[kk][i] = q.y;
+        rsn[kk][i] = q.z;
       }
       fW[i] += VM;
-      fR[i] += sV;
-      fS[i] += sV;
+      fQ[i] += V;
     }
   };
-  // per scenario: incentive and liquid bond_alpha of the epoch in use, each
+  // per scenario: incentive (and liquid bond_alpha) of the epoch in use, each
   // refilled with the next epoch's as soon as it is consumed
   float ri[K][4], rba[K][4];
   const float* fI[K];
   const float* fB[K];
-  float* pD[K];  // this epoch's dividend partials (lane's first row)
-  float* pH[K];  // this epoch's bond history (lane's first row), if stored
+  float* pD[K];  // this epoch's dividend partials
+  float* pH[K];  // this epoch's bond history, if stored
   const bool hist = A.B_hist != nullptr;
 #pragma unroll
   for (int k = 0; k < K; ++k) {
@@ -2455,7 +3085,7 @@ __global__ __launch_bounds__(256, kGrpWaves) void k_bonds_grp(BondArgs A) {
       ri[k][1] = x.y;
       ri[k][2] = x.z;
       ri[k][3] = x.w;
-      if (liquid_mask & (1u << k)) {
+      if (LIQ && ((liquid_mask >> k) & 1u)) {
         const float4 y = *reinterpret_cast<const float4*>(fB[k]);
         rba[k][0] = y.x;
         rba[k][1] = y.y;
@@ -2470,18 +3100,17 @@ __global__ __launch_bounds__(256, kGrpWaves) void k_bonds_grp(BondArgs A) {
   for (int kk = 0; kk < P; ++kk) fetch(kk, A.t0 + kk < A.t1);
 #pragma unroll
   for (int k = 0; k < K; ++k) fetch_s(k, true);
-  // Fixed-alpha scenarios: bond_alpha sits in rba for the whole scan (the
-  // per-element selects between the liquid and the fixed operands go), and
-  // one_minus_bond_alpha = (1 - bond_alpha) + p_corr. Both terms of p_corr
-  // are fp32 roundings of 1 - bond_alpha within 2^-25 of each other, so
-  // their difference is exact (Sterbenz, or one of them is 0) and adding it
-  // back to 1 - bond_alpha gives one_minus_bond_alpha bit for bit
+  // Liquid blocks: a fixed-alpha scenario keeps bond_alpha in rba for the
+  // whole scan, and one_minus_bond_alpha = (1 - bond_alpha) + p_corr. Both
+  // terms of p_corr are fp32 roundings of 1 - bond_alpha within 2^-25 of each
+  // other, so their difference is exact (Sterbenz, or one of them is 0) and
+  // adding it back to 1 - bond_alpha gives one_minus_bond_alpha bit for bit
   // (tests/test_host.py::test_grp_one_minus_alpha_correction).
   float p_corr[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     p_corr[k] = 0.0f;
-    if (!((liquid_mask >> k) & 1u)) {
+    if (LIQ && !((liquid_mask >> k) & 1u)) {
       p_corr[k] = p_omba[k] - (1.0f - p_ba[k]);
       if (p_corr[k] != p_corr[k]) p_corr[k] = 0.0f;  // bond_alpha = +-inf: -+inf + 0
 #pragma unroll
@@ -2494,18 +3123,28 @@ __global__ __launch_bounds__(256, kGrpWaves) void k_bonds_grp(BondArgs A) {
     for (int kk = 0; kk < P; ++kk) {
       const int t = tb + kk;
       if (t >= A.t1) break;
-      // normalised weights, once for the K scenarios
+      // normalised weights, once for the K scenarios: div_fast_nz's result
+      // from the stored reciprocal when every row of the wave is in range,
+      // else IEEE division (the same values up to the sign of a zero)
       float wn[R][4];
+      bool fast = true;
 #pragma unroll
-      for (int i = 0; i < R; ++i) {
-        const RowDiv rdv = row_div(rd[kk][i]);
-        bool slow = false;
+      for (int i = 0; i < R; ++i) fast &= rq[kk][i] == rq[kk][i];
+      if (__all(fast)) {
 #pragma unroll
-        for (int c = 0; c < 4; ++c) wn[i][c] = div_fast_nz(rw[kk][i][c], rdv, slow);
-        if (__any(slow)) {
+        for (int i = 0; i < R; ++i)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            const float a = rw[kk][i][c];
+            const float q = a * rq[kk][i];
+            const float e = fmaf(-rd[kk][i], q, a);
+            wn[i][c] = fmaf(e, rq[kk][i], q);
+          }
+      } else {
+#pragma unroll
+        for (int i = 0; i < R; ++i)
 #pragma unroll
           for (int c = 0; c < 4; ++c) wn[i][c] = rw[kk][i][c] / rd[kk][i];
-        }
       }
       float sv[R];
 #pragma unroll
@@ -2533,11 +3172,16 @@ __global__ __launch_bounds__(256, kGrpWaves) void k_bonds_grp(BondArgs A) {
         float bac[4], omba[4], ic[4];
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
-          // rba holds bond_alpha for a fixed-alpha scenario; p_corr turns
-          // 1 - rba into its (double-derived) one_minus_bond_alpha exactly
-          // and is +0 for a liquid one (see the set-up above)
-          bac[c] = rba[k][c];
-          omba[c] = (1.0f - rba[k][c]) + p_corr[k];
+          if (LIQ) {
+            // rba holds bond_alpha for a fixed-alpha scenario; p_corr turns
+            // 1 - rba into its (double-derived) one_minus_bond_alpha exactly
+            // and is +0 for a liquid one (see the set-up above)
+            bac[c] = rba[k][c];
+            omba[c] = (1.0f - rba[k][c]) + p_corr[k];
+          } else {
+            bac[c] = p_ba[k];
+            omba[c] = p_omba[k];
+          }
           ic[c] = ri[k][c];
         }
         fetch_s(k, t + 1 < A.t1);
@@ -2591,6 +3235,19 @@ __global__ __launch_bounds__(256, kGrpWaves) void k_bonds_grp(BondArgs A) {
   }
 }
 
+template <int VARIANT, int K, int R, int P>
+__global__ __launch_bounds__(256, kGrpWaves) void k_bonds_grp(BondArgs A) {
+  const int n0 = (blockIdx.x / (A.tiles * A.rowblocks)) * K;
+  unsigned liquid_mask = 0;
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+    if (n0 + k < A.N && A.prm[n0 + k].liquid_mode != YUMA_LIQUID_OFF) liquid_mask |= 1u << k;
+  if (VARIANT == YUMA_VARIANT_YUMA4 && liquid_mask != 0)  // block-uniform; Yuma3 has no bond_alpha
+    grp_scan<VARIANT, K, R, P, true>(A, liquid_mask);
+  else
+    grp_scan<VARIANT, K, R, P, false>(A, 0u);
+}
+
 // ---------------------------------------------------------------------------
 // Finalize, one block per slice: D = sum over tiles of the partials (Yuma4:
 // D = S * that, yumas.py:590), D_normalized = D / (D.sum() + 1e-6), and
@@ -2602,7 +3259,7 @@ __global__ __launch_bounds__(256) void k_finalize(const float* __restrict__ dpar
                                                   const float* __restrict__ tvc,
                                                   const float* __restrict__ tvn,
                                                   float* __restrict__ Dn, float* __restrict__ D,
-                                                  float* __restrict__ Tv, int dpl) {
+                                                  float* __restrict__ Tv, int dpl, int ttiles) {
   // thread (tg, vq): tile group tg = tid / 64 sums tiles tg, tg+4, ...; vq owns
   // validators 4vq..4vq+3 of the current 256-validator window. Fixed order:
   // per-group sequential, then groups 0..3.
@@ -2689,9 +3346,9 @@ __global__ __launch_bounds__(256) void k_finalize(const float* __restrict__ dpar
     if (D != nullptr) D[slice * V + v] = dsh[v];
     if (Tv != nullptr) {
       float a = 0.0f, b = 0.0f;
-      for (int k = 0; k < tiles; ++k) {
-        a = a + tvc[(slice * tiles + k) * V + v];
-        b = b + tvn[(slice * tiles + k) * V + v];
+      for (int k = 0; k < ttiles; ++k) {
+        a = a + tvc[(slice * ttiles + k) * V + v];
+        b = b + tvn[(slice * ttiles + k) * V + v];
       }
       Tv[slice * V + v] = a / b;
     }
@@ -2709,23 +3366,19 @@ __global__ __launch_bounds__(256) void k_add_eps(const float* __restrict__ rowsu
   for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256)
     rsd[i] = rowsum[i] + 1e-6f;
 }
-// per slice: sum over this shard's columns of C_raw (fp32; YumaRust fp64)
+// per slice: sum over this shard's columns of C_raw (fp32; YumaRust fp64),
+// in the canonical order over the shard's tiles (csum_canonical)
 __global__ __launch_bounds__(256) void k_csum(const double* __restrict__ craw, int rust, int M,
                                               float* __restrict__ csum_f,
                                               double* __restrict__ csum_d) {
-  __shared__ float redf[4];
-  __shared__ double redd[4];
+  __shared__ double stage[kCsumStage + 1];
   const long long slice = blockIdx.x;
   const double* cr = craw + slice * M;
   if (rust) {
-    double acc = 0.0;
-    for (int m = threadIdx.x; m < M; m += 256) acc = acc + cr[m];
-    acc = block_sum_d<256>(acc, redd);
+    const double acc = csum_canonical<double, 256>(cr, M, stage);
     if (threadIdx.x == 0) csum_d[slice] = acc;
   } else {
-    float acc = 0.0f;
-    for (int m = threadIdx.x; m < M; m += 256) acc = acc + (float)cr[m];
-    acc = block_sum<256>(acc, redf);
+    const float acc = csum_canonical<float, 256>(cr, M, reinterpret_cast<float*>(stage));
     if (threadIdx.x == 0) csum_f[slice] = acc;
   }
 }
@@ -2811,6 +3464,7 @@ size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
 struct Workspace {
   float* rsd;
+  float4* rq4;  // per input slice and row: {row sum, RN(1 / row sum) or NaN, stake, 0} (k_rowsum)
   int* sx;  // per slice: exact stake units or -1 (k_rowsum)
   float* sn;
   double* craw;
@@ -2828,11 +3482,20 @@ struct Workspace {
   float* sumc_f;
   double* sumc_d;
   int* crep;  // per scenario: consensus class representative (k_classes)
+  double* ctile;  // k_cons_rank: C_raw tile sums [slice][tile]
+  int* cnt;       // k_cons_rank: per-slice publish counters
+  int* err;       // k_cons_rank: a wait ran out
   size_t bytes;
 };
 
+// dividend-partial granularity of the bond scan: 64-miner tiles, or the
+// column-normalised scan's 16-miner strips (k_bonds_cn)
+size_t partial_tiles(int variant, int M) {
+  return variant <= YUMA_VARIANT_YUMA2 ? (size_t)(M + yk::kCnStrip - 1) / yk::kCnStrip
+                                       : (size_t)(M + yk::kTileM - 1) / yk::kTileM;
+}
+
 Workspace carve(char* base, int variant, int N, int E, int V, int M, int full) {
-  (void)variant;
   Workspace w{};
   const size_t S = (size_t)E * N;
   const size_t tiles = (size_t)(M + yk::kTileM - 1) / yk::kTileM;
@@ -2843,6 +3506,7 @@ Workspace carve(char* base, int variant, int N, int E, int V, int M, int full) {
     return p;
   };
   w.rsd = (float*)take(S * V * 4);
+  w.rq4 = (float4*)take(S * V * 16);
   w.sx = (int*)take(S * 4);
   w.sn = (float*)take(S * V * 4);
   w.craw = (double*)take(S * M * 8);
@@ -2852,7 +3516,7 @@ Workspace carve(char* base, int variant, int N, int E, int V, int M, int full) {
   w.I = (float*)take(S * M * 4);
   w.ba = (float*)take(S * M * 4);
   w.rpart = (float*)take(S * tiles * 4);
-  w.dpart = (float*)take(S * tiles * V * 4);
+  w.dpart = (float*)take(S * partial_tiles(variant, M) * V * 4);
   w.scal = (float*)take(S * 8 * 4);
   w.tvc = full ? (float*)take(S * tiles * V * 4) : nullptr;
   w.tvn = full ? (float*)take(S * tiles * V * 4) : nullptr;
@@ -2860,6 +3524,9 @@ Workspace carve(char* base, int variant, int N, int E, int V, int M, int full) {
   w.sumc_f = (float*)take(S * 4);
   w.sumc_d = (double*)take(S * 8);
   w.crep = (int*)take((size_t)N * 4);
+  w.ctile = (double*)take(S * tiles * 8);
+  w.cnt = (int*)take(S * 4);
+  w.err = (int*)take(4);
   w.bytes = off;
   return w;
 }
@@ -2934,9 +3601,13 @@ void launch_rank(RowCfg rc, long long nblocks, hipStream_t st, const float* W, c
                  int V, int M, long long slice0, int tiles, float* R, float* rpart, float* Wn,
                  float* Wc, float* tvc, float* tvn, int wsh, const int* crep = nullptr) {
   const bool full = Wn != nullptr || Wc != nullptr || tvc != nullptr;
-  if (!full && !yuma2) {  // streaming rank; k_rank_w also materialises Wn / Wc / T_v or clips W_prev
-    YK_LAUNCH(yk::k_rank_s<VEC>, nblocks, 256, st, W, rsd, sn, C, N, V, M, slice0, tiles, R, rpart,
-              wsh, crep);
+  if (!full) {  // streaming rank; k_rank_w also materialises Wn / Wc / T_v
+    if (yuma2)  // per scenario: W_prev (the caller's) is not shared by a consensus class
+      YK_LAUNCH((yk::k_rank_s<VEC, true>), nblocks, 256, st, W, rsd, sn, C, N, V, M, slice0, tiles, R,
+                rpart, wsh, nullptr, Wprev_init);
+    else
+      YK_LAUNCH((yk::k_rank_s<VEC, false>), nblocks, 256, st, W, rsd, sn, C, N, V, M, slice0, tiles, R,
+                rpart, wsh, crep, nullptr);
     return;
   }
   auto go = [&](auto kern) {
@@ -2983,9 +3654,31 @@ void launch_rank(RowCfg rc, long long nblocks, hipStream_t st, const float* W, c
 }
 
 // Column-normalised variants (Rust / Yuma1 / Yuma2): one block owns whole
-// 64-miner columns (single row block). Returns the dividend-partial layout.
+// columns (single row block). Run outputs of subnets above 64 validators take
+// the strip scan k_bonds_cn (16-miner strips, 8 waves, epochs in flight);
+// small subnets and the full-output epoch (W_b / instantaneous bonds stored)
+// k_bonds on 64-miner tiles. Returns the dividend-partial layout and sets
+// *ptiles to the partials per (slice, validator).
+template <int VARIANT, int R>
+int launch_cn(hipStream_t st, yk::BondArgs& A, int* ptiles) {
+  A.rowblocks = 1;
+  A.cblocks = (A.M + yk::kCnStrip - 1) / yk::kCnStrip;
+  *ptiles = A.cblocks;
+  const long long nblocks = (long long)A.N * A.cblocks;
+  YK_LAUNCH((yk::k_bonds_cn<VARIANT, R, R <= 2 ? 4 : (R == 4 ? 2 : 1)>), nblocks, 512, st, A);
+  return yk::DP_TV;
+}
 template <int VARIANT, bool VEC>
-int launch_bonds_colnorm(RowCfg rc, hipStream_t st, yk::BondArgs& A) {
+int launch_bonds_colnorm(RowCfg rc, hipStream_t st, yk::BondArgs& A, int* ptiles) {
+  if constexpr (VEC) {
+    if (A.V > 64 && A.Wb_out == nullptr && A.Binst_out == nullptr) {
+      if (A.V <= 128) return launch_cn<VARIANT, 1>(st, A, ptiles);
+      if (A.V <= 256) return launch_cn<VARIANT, 2>(st, A, ptiles);
+      if (A.V <= 512) return launch_cn<VARIANT, 4>(st, A, ptiles);
+      return launch_cn<VARIANT, 8>(st, A, ptiles);
+    }
+  }
+  *ptiles = A.tiles;
   A.rowblocks = 1;
   A.cblocks = A.tiles;
   const long long nblocks = (long long)A.N * A.tiles;
@@ -3040,7 +3733,7 @@ int launch_bonds_elem(hipStream_t st, yk::BondArgs& A) {
       return launch_elem_shape<VARIANT, 2, true, kWideP, true, true, 512, 1024, yk::DP_VT>(st, A);
   }
   if constexpr (VEC) {
-    if (A.wsh && A.N >= 2) {  // a sweep over one input trajectory
+    if (A.wsh && A.N >= 2 && A.rq4 != nullptr) {  // a sweep over one input trajectory
       constexpr int K = kScanGroup, R = 1;
       A.rowblocks = (A.V + 16 * R - 1) / (16 * R);
       A.cblocks = A.tiles;
@@ -3058,14 +3751,15 @@ int launch_bonds_elem(hipStream_t st, yk::BondArgs& A) {
 // Launch the bond scan for A.N scenarios over epochs [A.t0, A.t1); returns
 // the layout of the dividend partials it wrote (k_finalize / k_dsum read it).
 template <bool VEC>
-int launch_bonds(int variant, RowCfg rc, hipStream_t st, yk::BondArgs& A) {
+int launch_bonds(int variant, RowCfg rc, hipStream_t st, yk::BondArgs& A, int* ptiles) {
+  *ptiles = A.tiles;
   switch (variant) {
     case YUMA_VARIANT_RUST:
-      return launch_bonds_colnorm<YUMA_VARIANT_RUST, VEC>(rc, st, A);
+      return launch_bonds_colnorm<YUMA_VARIANT_RUST, VEC>(rc, st, A, ptiles);
     case YUMA_VARIANT_YUMA1:
-      return launch_bonds_colnorm<YUMA_VARIANT_YUMA1, VEC>(rc, st, A);
+      return launch_bonds_colnorm<YUMA_VARIANT_YUMA1, VEC>(rc, st, A, ptiles);
     case YUMA_VARIANT_YUMA2:
-      return launch_bonds_colnorm<YUMA_VARIANT_YUMA2, VEC>(rc, st, A);
+      return launch_bonds_colnorm<YUMA_VARIANT_YUMA2, VEC>(rc, st, A, ptiles);
     case YUMA_VARIANT_YUMA3:
       return launch_bonds_elem<YUMA_VARIANT_YUMA3, VEC>(st, A);
     default:
@@ -3094,6 +3788,21 @@ struct PhaseTimer {
     label.push_back(phase);
   }
 };
+
+// Persistent grid of k_cons_rank: as many blocks as fit on the device at
+// once, rounded down to whole slices of tiles (so a slice's tiles are one
+// round); 0 when a slice has more tiles than that (the multi-pass path).
+long long cons_rank_grid(bool rust, int tiles) {
+  int dev = 0, cus = 0, nb = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return 0;
+  const hipError_t e = rust ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, yk::k_cons_rank<true>, 256, 0)
+                            : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, yk::k_cons_rank<false>, 256, 0);
+  if (e != hipSuccess || nb < 1) return 0;
+  const long long cap = (long long)nb * cus;
+  return cap >= tiles ? cap / tiles * tiles : 0;
+}
 
 int run_impl(int variant, const yuma_params_t* prm, int N, int E, int V, int M, const float* W,
              const float* S, const float* B_init, const float* Wprev_init,
@@ -3148,8 +3857,14 @@ int run_impl(int variant, const yuma_params_t* prm, int N, int E, int V, int M, 
     crep = ws.crep;
   }
   const bool rank_stream = out->Wn == nullptr && out->Wc == nullptr && ws.tvc == nullptr &&
-                           variant != YUMA_VARIANT_YUMA2;
+                           variant != YUMA_VARIANT_YUMA2;  // Yuma2's W_prev: rank per scenario
   const int* rcrep = rank_stream ? crep : nullptr;
+  // consensus + quantisation + rank from one read of W (k_cons_rank): run
+  // outputs of 65-256 validators, whole 64-miner tiles, no consensus classes
+  const bool rust = variant == YUMA_VARIANT_RUST;
+  long long cr_grid = 0;
+  if (vec && rank_stream && crep == nullptr && rc == RC_256_16 && M % yk::kTileM == 0)
+    cr_grid = cons_rank_grid(rust, tiles);
 
   PhaseTimer tm{};
   tm.ms = phase_ms;
@@ -3169,28 +3884,45 @@ int run_impl(int variant, const yuma_params_t* prm, int N, int E, int V, int M, 
       tm.mark(YUMA_PHASE_ROWSUM);
       if (wide && vec)
         YK_LAUNCH((yk::k_rowsum<true, true>), rs_in * V, 256, st, W, S, V, M, rs_s0, V, ws.rsd,
-                  ws.sn, 0, ws.sx, fan);
+                  ws.sn, 0, ws.sx, fan, ws.rq4);
       else if (wide)
         YK_LAUNCH((yk::k_rowsum<false, true>), rs_in * V, 256, st, W, S, V, M, rs_s0, V, ws.rsd,
-                  ws.sn, 0, ws.sx, fan);
+                  ws.sn, 0, ws.sx, fan, ws.rq4);
       else if (vec)
         YK_LAUNCH(yk::k_rowsum<true>, rs_in * rowblocks4, 256, st, W, S, V, M, rs_s0, rowblocks4,
-                  ws.rsd, ws.sn, 0, ws.sx, fan);
+                  ws.rsd, ws.sn, 0, ws.sx, fan, ws.rq4);
       else
         YK_LAUNCH(yk::k_rowsum<false>, rs_in * rowblocks4, 256, st, W, S, V, M, rs_s0,
-                  rowblocks4, ws.rsd, ws.sn, 0, ws.sx, fan);
+                  rowblocks4, ws.rsd, ws.sn, 0, ws.sx, fan, ws.rq4);
       tm.mark(YUMA_PHASE_CONSENSUS);
-      if (vec)
+      if (cr_grid > 0) {
+        (void)hipMemsetAsync(ws.cnt, 0, (size_t)ns * 4, st);
+        (void)hipMemsetAsync(ws.err, 0, 4, st);
+        yk::ConsRankArgs CA{W, ws.rsd, ws.sn, ws.sx, prm, out->P, C, ws.qlev, Rr, ws.rpart, ws.ctile,
+                            ws.cnt, ws.sumc_f, ws.sumc_d, ws.err, s0, ns, N, V, M, tiles};
+        const long long g = cr_grid < ns * tiles ? cr_grid : ns * tiles;
+        if (rust)
+          YK_LAUNCH(yk::k_cons_rank<true>, g, 256, st, CA);
+        else
+          YK_LAUNCH(yk::k_cons_rank<false>, g, 256, st, CA);
+        tm.mark(YUMA_PHASE_QUANTISE);  // liquid alpha: quantiles of the levels
+        YK_LAUNCH(yk::k_liquid<256>, ns, 256, st, prm, N, M, s0, C, ws.qlev, M, ba_buf, ws.scal,
+                  ws.sumc_f, ws.sumc_d, rust ? 1 : 0);
+      } else if (vec)
         launch_consensus<true>(rc, ns * tiles, st, W, ws.rsd, ws.sn, ws.sx, prm, N, V, M, s0, tiles,
                                ws.craw, out->P, wsh, crep);
       else
         launch_consensus<false>(rc, ns * tiles, st, W, ws.rsd, ws.sn, ws.sx, prm, N, V, M, s0,
                                 tiles, ws.craw, out->P, wsh, crep);
-      tm.mark(YUMA_PHASE_QUANTISE);
-      YK_LAUNCH(yk::k_quantise<256>, ns, 256, st, ws.craw, prm, variant, N, M, s0, C, ws.qlev,
-                ba_buf, ws.scal, nullptr, nullptr, 0, crep);
+      if (cr_grid == 0) {
+        tm.mark(YUMA_PHASE_QUANTISE);
+        YK_LAUNCH(yk::k_quantise<256>, ns, 256, st, ws.craw, prm, variant, N, M, s0, C, ws.qlev,
+                  ba_buf, ws.scal, nullptr, nullptr, 0, crep);
+      }
       tm.mark(YUMA_PHASE_RANK);
-      if (vec)
+      if (cr_grid > 0) {
+        // ranked by k_cons_rank
+      } else if (vec)
         launch_rank<true>(rc, ns * tiles, st, W, ws.rsd, ws.sn, C, Wprev_init,
                           variant == YUMA_VARIANT_YUMA2, N, V, M, s0, tiles, Rr, ws.rpart, out->Wn,
                           out->Wc, ws.tvc, ws.tvn, wsh, rcrep);
@@ -3219,6 +3951,7 @@ int run_impl(int variant, const yuma_params_t* prm, int N, int E, int V, int M, 
     A.Wb_out = out->Wb;
     A.Binst_out = out->B_inst;
     A.dpart = ws.dpart;
+    A.rq4 = ws.rq4;
     A.N = N;
     A.V = V;
     A.M = M;
@@ -3227,10 +3960,12 @@ int run_impl(int variant, const yuma_params_t* prm, int N, int E, int V, int M, 
     A.t1 = c1;
     A.wsh = wsh;
     tm.mark(YUMA_PHASE_BONDS);
-    const int dpl = vec ? launch_bonds<true>(variant, rc, st, A) : launch_bonds<false>(variant, rc, st, A);
+    int ptiles = tiles;
+    const int dpl = vec ? launch_bonds<true>(variant, rc, st, A, &ptiles)
+                        : launch_bonds<false>(variant, rc, st, A, &ptiles);
     tm.mark(YUMA_PHASE_FINALIZE);
-    YK_LAUNCH(yk::k_finalize, ns, 256, st, ws.dpart, ws.sn, variant, V, s0, tiles, ws.tvc,
-              ws.tvn, out->Dn, out->D, out->Tv, dpl);
+    YK_LAUNCH(yk::k_finalize, ns, 256, st, ws.dpart, ws.sn, variant, V, s0, ptiles, ws.tvc,
+              ws.tvn, out->Dn, out->D, out->Tv, dpl, tiles);
     if (out->Sn != nullptr)
       (void)hipMemcpyAsync(out->Sn + s0 * V, ws.sn + s0 * V, (size_t)ns * V * 4,
                            hipMemcpyDeviceToDevice, st);
@@ -3306,10 +4041,10 @@ int shard_stage_impl(int stage, int variant, const yuma_params_t* prm, int N, in
       const int rb4 = (V + 3) / 4;
       if (vec)
         YK_LAUNCH(yk::k_rowsum<true>, ns * rb4, 256, st, W, S, V, M, 0LL, rb4, io->rowsum_part,
-                  ws.sn, 1, ws.sx, 1);
+                  ws.sn, 1, ws.sx, 1, (float4*)nullptr);
       else
         YK_LAUNCH(yk::k_rowsum<false>, ns * rb4, 256, st, W, S, V, M, 0LL, rb4, io->rowsum_part,
-                  ws.sn, 1, ws.sx, 1);
+                  ws.sn, 1, ws.sx, 1, (float4*)nullptr);
       break;
     }
     case 2: {
@@ -3380,8 +4115,10 @@ int shard_stage_impl(int stage, int variant, const yuma_params_t* prm, int N, in
       A.tiles = tiles;
       A.t0 = 0;
       A.t1 = E;
-      const int dpl = vec ? launch_bonds<true>(variant, rc, st, A) : launch_bonds<false>(variant, rc, st, A);
-      YK_LAUNCH(yk::k_dsum, ns, 256, st, ws.dpart, V, tiles, io->dsum_part, dpl);
+      int ptiles = tiles;
+      const int dpl = vec ? launch_bonds<true>(variant, rc, st, A, &ptiles)
+                          : launch_bonds<false>(variant, rc, st, A, &ptiles);
+      YK_LAUNCH(yk::k_dsum, ns, 256, st, ws.dpart, V, ptiles, io->dsum_part, dpl);
       break;
     }
     case 5: {
@@ -3389,7 +4126,7 @@ int shard_stage_impl(int stage, int variant, const yuma_params_t* prm, int N, in
       if (full && !io->tv) return fail(YUMA_EINVAL, "stage 5 with out->Tv needs io->tv");
       YK_LAUNCH(yk::k_finalize, ns, 256, st, io->dsum, ws.sn, variant, V, 0LL, 1,
                 full ? io->tv : nullptr, full ? io->tv + ns * V : nullptr, out->Dn, out->D,
-                out->Tv, (int)yk::DP_TV);
+                out->Tv, (int)yk::DP_TV, 1);
       if (out->Sn != nullptr)
         (void)hipMemcpyAsync(out->Sn, ws.sn, (size_t)ns * V * 4, hipMemcpyDeviceToDevice, st);
       if (out->alpha_ab != nullptr)
