@@ -38,3 +38,6 @@ PATCHES["cr_w3"] = [("__global__ __launch_bounds__(256, 2) void k_cons_rank", "_
 PATCHES["cr_w4"] = [("__global__ __launch_bounds__(256, 2) void k_cons_rank", "__global__ __launch_bounds__(256, 4) void k_cons_rank")]
 # the multi-pass path (k_consensus_w + k_quantise + k_rank_s) with this source's orders
 PATCHES["cr_off"] = [("    cr_grid = cons_rank_grid(rust, tiles);", "    cr_grid = 0;")]
+PATCHES["grp_r2"] = [("      constexpr int K = kScanGroup, R = 1;", "      constexpr int K = kScanGroup, R = 2;")]
+PATCHES["grp_r2_w4"] = PATCHES["grp_r2"] + PATCHES["grp_w4"]
+PATCHES["grp_r2_w5"] = PATCHES["grp_r2"] + PATCHES["grp_w5"]

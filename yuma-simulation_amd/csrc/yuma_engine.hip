@@ -360,15 +360,22 @@ __device__ __forceinline__ void load4_vec(const float* __restrict__ v, int m, in
 constexpr int kWideChunks = 64, kMaxWideChunks = 4096;
 // RN(1 / rs) when div_fast of every weight of the row by rs takes its fast
 // path (|rs| and every nonzero |w| in [2^-60, 2^60]; bmax / bmin1: the row's
-// max |w| and min nonzero |w| - 1 as bit patterns), else NaN: the sweep scan
-// then divides without a per-element guard (k_bonds_grp). k_rowsum stores it
-// per INPUT slice and row as rq4 = {row sum, this, normalised stake, 0}: one
-// 16-byte load per row and epoch.
+// max |w| and min nonzero |w| - 1 as bit patterns), else NaN: the bond scans
+// then divide without a per-row reciprocal or a per-element guard
+// (k_bonds_elem, k_bonds_grp). k_rowsum stores it per INPUT slice and row as
+// rq4 = {row sum, this, normalised stake, 0}: one 16-byte load per row and
+// epoch.
+__device__ __forceinline__ bool screen_ok(unsigned bmax, unsigned bmin1) {
+  return bmax <= __float_as_uint(0x1p60f) && (bmin1 == 0xFFFFFFFFu || bmin1 + 1u >= __float_as_uint(0x1p-60f));
+}
 __device__ __forceinline__ float fast_row_rcp(float rs, unsigned bmax, unsigned bmin1) {
   const float ad = fabsf(rs);
-  const bool ok = ad >= 0x1p-60f && ad <= 0x1p60f && bmax <= __float_as_uint(0x1p60f) &&
-                  (bmin1 == 0xFFFFFFFFu || bmin1 + 1u >= __float_as_uint(0x1p-60f));
-  return ok ? 1.0f / rs : qnan();
+  return ad >= 0x1p-60f && ad <= 0x1p60f && screen_ok(bmax, bmin1) ? 1.0f / rs : qnan();
+}
+// a column shard's row (partial row sum): 1 when its own weights pass the
+// screen, else NaN; k_add_eps completes it once the row sum is known
+__device__ __forceinline__ float screen_mark(unsigned bmax, unsigned bmin1) {
+  return screen_ok(bmax, bmin1) ? 1.0f : qnan();
 }
 template <bool VEC, bool WIDE = false>
 __global__ __launch_bounds__(256) void k_rowsum(const float* __restrict__ W,
@@ -444,7 +451,8 @@ __global__ __launch_bounds__(256) void k_rowsum(const float* __restrict__ W,
           bx = max(bx, qb[0][w]);
           bn = min(bn, qb[1][w]);
         }
-        *reinterpret_cast<float2*>(&rq4[wsl * V + rb]) = make_float2(rs, fast_row_rcp(rs, bx, bn));
+        *reinterpret_cast<float2*>(&rq4[wsl * V + rb]) =
+            make_float2(rs, partial ? screen_mark(bx, bn) : fast_row_rcp(rs, bx, bn));
       }
     }
   }
@@ -484,7 +492,8 @@ __global__ __launch_bounds__(256) void k_rowsum(const float* __restrict__ W,
         bmin1 = min(bmin1, (unsigned)__shfl_xor((int)bmin1, o, 64));
       }
       if (lane == 0)
-        *reinterpret_cast<float2*>(&rq4[wsl * V + row]) = make_float2(rs, fast_row_rcp(rs, bmax, bmin1));
+        *reinterpret_cast<float2*>(&rq4[wsl * V + row]) =
+            make_float2(rs, partial ? screen_mark(bmax, bmin1) : fast_row_rcp(rs, bmax, bmin1));
     }
   }
   // the stake normalisation: output slices f = rb, rb + rowblocks, ... of
@@ -1279,7 +1288,11 @@ __global__ __launch_bounds__(256, 4) void k_consensus_w(const float* __restrict_
 // Per item the block runs k_consensus_w's load / normalisation / prerank /
 // search with the tile resident in registers and publishes the tile's C_raw
 // sum (an agent-scope counter per slice; the slice's last tile adds the tile
-// sums in order: csum_canonical's ΣC). One round later — while its next
+// sums in order: csum_canonical's ΣC). The hand-offs follow the guide's
+// sc1 protocol (MI355X_MICROARCH.md, inter-workgroup visibility, first row):
+// payloads stored and loaded sc1 (relaxed agent atomics), the storing wave's
+// vmcnt(0) before a relaxed agent add, relaxed sc1 polls — no L2 write-back
+// or L1 invalidate per item. One round later — while its next
 // item's W is in flight — it quantises its previous tile's columns with that
 // ΣC (k_quantise's formula) and ranks them from the tile still in registers
 // (two register sets, alternating), in k_rank_s's summation order. So the
@@ -1340,7 +1353,7 @@ __global__ __launch_bounds__(256, 2) void k_cons_rank(ConsRankArgs A) {
       const int pn = (int)(ps % N);
       const int iters = A.prm[pn].bisect_iters;
       if (__hip_atomic_load(A.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
-        for (int spin = 0; __hip_atomic_load(A.cnt + pr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) <= tiles;) {
+        for (int spin = 0; __hip_atomic_load(A.cnt + pr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <= tiles;) {
           __builtin_amdgcn_s_sleep(1);
           if (++spin > kConsRankSpin) {  // never expected; later waits are skipped
             __hip_atomic_store(A.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1505,7 +1518,8 @@ __global__ __launch_bounds__(256, 2) void k_cons_rank(ConsRankArgs A) {
         const long long sr = slice - A.slice0;
         const T ts = (tred[par][0] + tred[par][1]) + (tred[par][2] + tred[par][3]);
         __hip_atomic_store(A.ctile + sr * tiles + tile, (double)ts, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int old = __hip_atomic_fetch_add(A.cnt + sr, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the sc1 store has left before the add
+        const int old = __hip_atomic_fetch_add(A.cnt + sr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (old == tiles - 1) {  // the slice's last tile: ΣC, tiles in order
           T tot = (T)0;
           for (int k = 0; k < tiles; ++k)
@@ -1514,7 +1528,8 @@ __global__ __launch_bounds__(256, 2) void k_cons_rank(ConsRankArgs A) {
             __hip_atomic_store(A.sumc_d + sr, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           else
             __hip_atomic_store(A.sumc_f + sr, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __hip_atomic_fetch_add(A.cnt + sr, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          __hip_atomic_fetch_add(A.cnt + sr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
       }
     }
@@ -2820,15 +2835,18 @@ __global__ __launch_bounds__(BS, 1) void k_bonds_elem(BondArgs A) {
     }
   }
 
-  float rw[P][R][4], rd[P][R], rsn[P][R], ri[P][4], rba[P][4];
+  float rw[P][R][4], rd[P][R], rq[P][R], rsn[P][R], ri[P][4], rba[P][4];
   auto fetch = [&](int k, int t) {
     const long long slice = (long long)t * N + n;
+    const long long wsl = A.wsh ? (long long)t : slice;
 #pragma unroll
     for (int i = 0; i < R; ++i) {
       const int rr = min(row0 + G * i, V - 1);
-      load4c<VEC>(A.W + (A.wsh ? (long long)t : slice) * VM, rr, V, m, M, rw[k][i]);
-      rd[k][i] = A.rsd[slice * V + rr];
-      rsn[k][i] = A.sn[slice * V + rr];
+      load4c<VEC>(A.W + wsl * VM, rr, V, m, M, rw[k][i]);
+      const float4 q = A.rq4[wsl * V + rr];  // {row sum, reciprocal or NaN, stake, 0}
+      rd[k][i] = q.x;
+      rq[k][i] = q.y;
+      rsn[k][i] = q.z;
     }
     // columns >= M never reach an output
     if (VECI) {
@@ -2884,13 +2902,20 @@ __global__ __launch_bounds__(BS, 1) void k_bonds_elem(BondArgs A) {
         constexpr bool SHORT = !(VARIANT == YUMA_VARIANT_YUMA4 && NT);
         auto mn = [](float a, float b) { return SHORT ? vmin(a, b) : tmin(a, b); };
         auto mx = [](float a, float b) { return SHORT ? vmax(a, b) : tmax(a, b); };
+        // div_fast(_nz)'s result from k_rowsum's screened reciprocal when
+        // every row of the wave passed the screen, else IEEE (same values
+        // up to the sign of a zero, which SHORT forms cannot show)
         float wn[4];
-        const RowDiv rdv = row_div(rd[k][i]);
-        bool slow = false;
+        if (__all(rq[k][i] == rq[k][i])) {
 #pragma unroll
-        for (int c = 0; c < 4; ++c)
-          wn[c] = SHORT ? div_fast_nz(rw[k][i][c], rdv, slow) : div_fast(rw[k][i][c], rdv, slow);
-        if (__any(slow)) {
+          for (int c = 0; c < 4; ++c) {
+            const float a = rw[k][i][c];
+            const float q = a * rq[k][i];
+            const float e = fmaf(-rd[k][i], q, a);
+            const float q1 = fmaf(e, rq[k][i], q);
+            wn[c] = SHORT ? q1 : (a == 0.0f ? q : q1);
+          }
+        } else {
 #pragma unroll
           for (int c = 0; c < 4; ++c) wn[c] = rw[k][i][c] / rd[k][i];
         }
@@ -3361,10 +3386,18 @@ __global__ __launch_bounds__(256) void k_finalize(const float* __restrict__ dpar
 // reduced values. Each partial is a fixed-order sum over this shard's columns.
 // ---------------------------------------------------------------------------
 // rsd = (sum of the shards' row sums) + 1e-6 (yumas.py:186)
+// and rq4 = {row sum, RN(1 / row sum) or NaN, stake, 0} from stage 1's screen mark
 __global__ __launch_bounds__(256) void k_add_eps(const float* __restrict__ rowsum, long long n,
-                                                 float* __restrict__ rsd) {
-  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256)
-    rsd[i] = rowsum[i] + 1e-6f;
+                                                 float* __restrict__ rsd, float4* __restrict__ rq4) {
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    const float rs = rowsum[i] + 1e-6f;
+    rsd[i] = rs;
+    float4 q = rq4[i];
+    const float ad = fabsf(rs);
+    q.x = rs;
+    q.y = q.y == q.y && ad >= 0x1p-60f && ad <= 0x1p60f ? 1.0f / rs : qnan();
+    rq4[i] = q;
+  }
 }
 // per slice: sum over this shard's columns of C_raw (fp32; YumaRust fp64),
 // in the canonical order over the shard's tiles (csum_canonical)
@@ -4041,10 +4074,10 @@ int shard_stage_impl(int stage, int variant, const yuma_params_t* prm, int N, in
       const int rb4 = (V + 3) / 4;
       if (vec)
         YK_LAUNCH(yk::k_rowsum<true>, ns * rb4, 256, st, W, S, V, M, 0LL, rb4, io->rowsum_part,
-                  ws.sn, 1, ws.sx, 1, (float4*)nullptr);
+                  ws.sn, 1, ws.sx, 1, ws.rq4);
       else
         YK_LAUNCH(yk::k_rowsum<false>, ns * rb4, 256, st, W, S, V, M, 0LL, rb4, io->rowsum_part,
-                  ws.sn, 1, ws.sx, 1, (float4*)nullptr);
+                  ws.sn, 1, ws.sx, 1, ws.rq4);
       break;
     }
     case 2: {
@@ -4052,7 +4085,7 @@ int shard_stage_impl(int stage, int variant, const yuma_params_t* prm, int N, in
         return fail(YUMA_EINVAL, "stage 2 needs io->rowsum and io->csum_part%s", rust ? "_d" : "");
       long long nb = (ns * V + 255) / 256;
       if (nb > 4096) nb = 4096;
-      YK_LAUNCH(yk::k_add_eps, nb, 256, st, io->rowsum, ns * V, ws.rsd);
+      YK_LAUNCH(yk::k_add_eps, nb, 256, st, io->rowsum, ns * V, ws.rsd, ws.rq4);
       if (vec)
         launch_consensus<true>(rc, ns * tiles, st, W, ws.rsd, ws.sn, ws.sx, prm, N, V, M, 0LL, tiles,
                                ws.craw, out->P, 0, nullptr);
@@ -4109,6 +4142,7 @@ int shard_stage_impl(int stage, int variant, const yuma_params_t* prm, int N, in
       A.Wb_out = out->Wb;
       A.Binst_out = out->B_inst;
       A.dpart = ws.dpart;
+      A.rq4 = ws.rq4;
       A.N = N;
       A.V = V;
       A.M = M;
