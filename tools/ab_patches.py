@@ -23,21 +23,20 @@ PATCHES = {
         "        d = wsum16(d);  // sum_row16's xor-butterfly tree, on DPP\n        if (d == 1.2345e-37f)\n        if")],
 }
 
-# k_bonds_grp (c3 sweep scan), round 4
-PATCHES["grp_w5"] = [("constexpr int kGrpWaves = 6;", "constexpr int kGrpWaves = 5;")]
-PATCHES["grp_w4"] = [("constexpr int kGrpWaves = 6;", "constexpr int kGrpWaves = 4;")]
-PATCHES["grp_noliqsplit"] = [(
+# k_bonds_grp (c3 sweep scan), round 4 (product: K = 2, R = 2, 4 waves / SIMD)
+PATCHES["grp_r1_w6"] = [("      constexpr int K = kScanGroup, R = 2;", "      constexpr int K = kScanGroup, R = 1;"),
+                        ("constexpr int kGrpWaves = 4;", "constexpr int kGrpWaves = 6;")]
+PATCHES["grp_r4_w2"] = [("      constexpr int K = kScanGroup, R = 2;", "      constexpr int K = kScanGroup, R = 4;"),
+                        ("constexpr int kGrpWaves = 4;", "constexpr int kGrpWaves = 2;")]
+PATCHES["grp_r2_w3"] = [("constexpr int kGrpWaves = 4;", "constexpr int kGrpWaves = 3;")]
+PATCHES["grp_k1_r4_w4"] = [("      constexpr int K = kScanGroup, R = 2;", "      constexpr int K = 1, R = 4;")]
+PATCHES["grp_r2_noliqsplit"] = [(
     "  if (VARIANT == YUMA_VARIANT_YUMA4 && liquid_mask != 0)  // block-uniform; Yuma3 has no bond_alpha\n"
     "    grp_scan<VARIANT, K, R, P, true>(A, liquid_mask);\n"
     "  else\n    grp_scan<VARIANT, K, R, P, false>(A, 0u);",
     "  grp_scan<VARIANT, K, R, P, true>(A, liquid_mask);")]
-PATCHES["grp_noliqsplit_w5"] = PATCHES["grp_noliqsplit"] + PATCHES["grp_w5"]
 
 # k_cons_rank (consensus + quantise + rank from one read of W), round 4
 PATCHES["cr_w3"] = [("__global__ __launch_bounds__(256, 2) void k_cons_rank", "__global__ __launch_bounds__(256, 3) void k_cons_rank")]
-PATCHES["cr_w4"] = [("__global__ __launch_bounds__(256, 2) void k_cons_rank", "__global__ __launch_bounds__(256, 4) void k_cons_rank")]
 # the multi-pass path (k_consensus_w + k_quantise + k_rank_s) with this source's orders
 PATCHES["cr_off"] = [("    cr_grid = cons_rank_grid(rust, tiles);", "    cr_grid = 0;")]
-PATCHES["grp_r2"] = [("      constexpr int K = kScanGroup, R = 1;", "      constexpr int K = kScanGroup, R = 2;")]
-PATCHES["grp_r2_w4"] = PATCHES["grp_r2"] + PATCHES["grp_w4"]
-PATCHES["grp_r2_w5"] = PATCHES["grp_r2"] + PATCHES["grp_w5"]

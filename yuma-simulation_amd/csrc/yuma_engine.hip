@@ -1321,7 +1321,7 @@ struct ConsRankArgs {
   int N, V, M, tiles;
 };
 
-constexpr int kConsRankSpin = 1 << 22;
+constexpr int kConsRankSpin = 1 << 20;
 
 template <bool RUST>
 __global__ __launch_bounds__(256, 2) void k_cons_rank(ConsRankArgs A) {
@@ -1331,6 +1331,7 @@ __global__ __launch_bounds__(256, 2) void k_cons_rank(ConsRankArgs A) {
   __shared__ __attribute__((aligned(16))) float rl[4][48 * R];
   __shared__ T tred[2][4];      // C_raw wave sums of the item being published
   __shared__ float rred[2][4];  // rank wave sums of the item being ranked
+  __shared__ T cst[512];        // a slice's C_raw tile sums (its last block; tiles <= 512)
   const WLay L = wlay();
   const int V = A.V, M = A.M, tiles = A.tiles, N = A.N;
   const long long items = A.nslices * tiles;
@@ -1352,15 +1353,18 @@ __global__ __launch_bounds__(256, 2) void k_cons_rank(ConsRankArgs A) {
       const int pm = pt * kTileM + L.wave * 16 + L.cq * 4;
       const int pn = (int)(ps % N);
       const int iters = A.prm[pn].bisect_iters;
-      if (__hip_atomic_load(A.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+      // ONE lane polls (sc1 loads); the block's other waves load ΣC after the
+      // barrier that lane's wave joins once its poll matched
+      if (threadIdx.x == 0 && __hip_atomic_load(A.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
         for (int spin = 0; __hip_atomic_load(A.cnt + pr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <= tiles;) {
-          __builtin_amdgcn_s_sleep(1);
+          __builtin_amdgcn_s_sleep(8);
           if (++spin > kConsRankSpin) {  // never expected; later waits are skipped
             __hip_atomic_store(A.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             break;
           }
         }
       }
+      lds_barrier();
       float Cq[4];
       int lev[4];
       const double top = (double)(1 << iters);
@@ -1514,22 +1518,34 @@ __global__ __launch_bounds__(256, 2) void k_cons_rank(ConsRankArgs A) {
       q = q + __shfl_xor(q, 32, 64);
       if (L.lane == 0) tred[par][L.wave] = q;
       lds_barrier();
-      if (threadIdx.x == 0) {
+      if (L.wave == 0) {
         const long long sr = slice - A.slice0;
-        const T ts = (tred[par][0] + tred[par][1]) + (tred[par][2] + tred[par][3]);
-        __hip_atomic_store(A.ctile + sr * tiles + tile, (double)ts, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the sc1 store has left before the add
-        const int old = __hip_atomic_fetch_add(A.cnt + sr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        int old = 0;
+        if (L.lane == 0) {
+          const T ts = (tred[par][0] + tred[par][1]) + (tred[par][2] + tred[par][3]);
+          __hip_atomic_store(A.ctile + sr * tiles + tile, (double)ts, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the sc1 store has left before the add
+          old = __hip_atomic_fetch_add(A.cnt + sr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        old = __shfl(old, 0, 64);
         if (old == tiles - 1) {  // the slice's last tile: ΣC, tiles in order
-          T tot = (T)0;
-          for (int k = 0; k < tiles; ++k)
-            tot = tot + (T)__hip_atomic_load(A.ctile + sr * tiles + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if constexpr (RUST)
-            __hip_atomic_store(A.sumc_d + sr, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          else
-            __hip_atomic_store(A.sumc_f + sr, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          __hip_atomic_fetch_add(A.cnt + sr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          // every tile sum in flight at once (sc1 loads, lane k: tiles k, k + 64, ...),
+          // parked in LDS, added in tile order by one lane
+          for (int k = L.lane; k < tiles; k += 64)
+            cst[k] = (T)__hip_atomic_load(A.ctile + sr * tiles + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          if (L.lane == 0) {
+            T tot = (T)0;
+            for (int k = 0; k < tiles; ++k) tot = tot + cst[k];
+            if constexpr (RUST)
+              __hip_atomic_store(A.sumc_d + sr, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            else
+              __hip_atomic_store(A.sumc_f + sr, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_fetch_add(A.cnt + sr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
         }
       }
     }
@@ -2843,10 +2859,15 @@ __global__ __launch_bounds__(BS, 1) void k_bonds_elem(BondArgs A) {
     for (int i = 0; i < R; ++i) {
       const int rr = min(row0 + G * i, V - 1);
       load4c<VEC>(A.W + wsl * VM, rr, V, m, M, rw[k][i]);
-      const float4 q = A.rq4[wsl * V + rr];  // {row sum, reciprocal or NaN, stake, 0}
-      rd[k][i] = q.x;
-      rq[k][i] = q.y;
-      rsn[k][i] = q.z;
+      if (NT) {  // the history scans: row sums and stakes, reciprocal per row
+        rd[k][i] = A.rsd[slice * V + rr];
+        rsn[k][i] = A.sn[slice * V + rr];
+      } else {
+        const float4 q = A.rq4[wsl * V + rr];  // {row sum, reciprocal or NaN, stake, 0}
+        rd[k][i] = q.x;
+        rq[k][i] = q.y;
+        rsn[k][i] = q.z;
+      }
     }
     // columns >= M never reach an output
     if (VECI) {
@@ -2904,9 +2925,21 @@ __global__ __launch_bounds__(BS, 1) void k_bonds_elem(BondArgs A) {
         auto mx = [](float a, float b) { return SHORT ? vmax(a, b) : tmax(a, b); };
         // div_fast(_nz)'s result from k_rowsum's screened reciprocal when
         // every row of the wave passed the screen, else IEEE (same values
-        // up to the sign of a zero, which SHORT forms cannot show)
+        // up to the sign of a zero, which SHORT forms cannot show). The
+        // history scans keep the per-row reciprocal and guard: with the
+        // stored reciprocal the c2 wide scan ran 1.58 -> 1.70 ms (same box).
         float wn[4];
-        if (__all(rq[k][i] == rq[k][i])) {
+        if (NT) {
+          const RowDiv rdv = row_div(rd[k][i]);
+          bool slow = false;
+#pragma unroll
+          for (int c = 0; c < 4; ++c)
+            wn[c] = SHORT ? div_fast_nz(rw[k][i][c], rdv, slow) : div_fast(rw[k][i][c], rdv, slow);
+          if (__any(slow)) {
+#pragma unroll
+            for (int c = 0; c < 4; ++c) wn[c] = rw[k][i][c] / rd[k][i];
+          }
+        } else if (__all(rq[k][i] == rq[k][i])) {
 #pragma unroll
           for (int c = 0; c < 4; ++c) {
             const float a = rw[k][i][c];
@@ -2999,7 +3032,7 @@ __global__ __launch_bounds__(BS, 1) void k_bonds_elem(BondArgs A) {
 // c3_scan_group_k.txt); packed-pair f32 math and an XCD-grouped block order
 // lost.
 // ---------------------------------------------------------------------------
-constexpr int kGrpWaves = 6;  // minimum waves per SIMD of the sweep scan
+constexpr int kGrpWaves = 4;  // minimum waves per SIMD of the sweep scan (R = 2: 120 VGPRs)
 template <int VARIANT, int K, int R, int P, bool LIQ>
 __device__ __forceinline__ void grp_scan(const BondArgs& A, unsigned liquid_mask) {
   constexpr int G = 16;
@@ -3767,7 +3800,7 @@ int launch_bonds_elem(hipStream_t st, yk::BondArgs& A) {
   }
   if constexpr (VEC) {
     if (A.wsh && A.N >= 2 && A.rq4 != nullptr) {  // a sweep over one input trajectory
-      constexpr int K = kScanGroup, R = 1;
+      constexpr int K = kScanGroup, R = 2;
       A.rowblocks = (A.V + 16 * R - 1) / (16 * R);
       A.cblocks = A.tiles;
       const long long nblocks = (long long)((A.N + K - 1) / K) * A.rowblocks * A.tiles;
@@ -3834,7 +3867,7 @@ long long cons_rank_grid(bool rust, int tiles) {
                             : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, yk::k_cons_rank<false>, 256, 0);
   if (e != hipSuccess || nb < 1) return 0;
   const long long cap = (long long)nb * cus;
-  return cap >= tiles ? cap / tiles * tiles : 0;
+  return cap >= tiles && tiles <= 512 ? cap / tiles * tiles : 0;  // 512: k_cons_rank's cst
 }
 
 int run_impl(int variant, const yuma_params_t* prm, int N, int E, int V, int M, const float* W,
