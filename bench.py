@@ -58,49 +58,28 @@ METRIC = "scenario-epochs/sec (256V x 4096M) at 1/8 GPUs; % of HBM peak GB/s"
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 
 
-def fused_cons_rank(variant: int, V: int, M: int, shared: bool = False, N: int = 1) -> bool:
-    """run_impl's k_cons_rank condition (yuma_engine.hip): consensus,
-    quantisation and rank from one read of W for run outputs of 65-256
-    validators in whole 64-miner tiles, without shared-input consensus
-    classes, not Yuma 2 (its rank clips W_prev), and a slice's tiles within
-    one persistent round (<= 512 blocks: 2 per CU on MI355X)."""
-    return (variant != 2 and 64 < V <= 256 and M % 64 == 0 and M // 64 <= 512
-            and not (shared and N > 1))
-
-
 def phase_bytes(phase: str, V: int, M: int, variant: int, liquid: bool, hist: bool, chunk: int,
-                wshare: int = 1, fused: bool = False) -> float:
+                wshare: int = 1) -> float:
     """Algorithmic HBM bytes one phase must move per scenario-epoch (each input
     read once, each output written once). DESIGN.md §Roofline tabulates them.
     wshare: scenarios reading one shared input trajectory (the c3 sweep): W
     and the per-epoch row sums are read once per input epoch for all of them,
-    so their bytes are divided among the wshare scenarios. fused: the
-    k_cons_rank path (consensus + quantisation + rank in the consensus phase,
-    the liquid-alpha quantiles in the quantise phase, no rank phase)."""
+    so their bytes are divided among the wshare scenarios."""
     tiles = (M + 63) // 64
     ptiles = (M + 15) // 16 if variant <= 2 else tiles  # dividend partials per (slice, validator)
     VM = V * M
     colnorm = variant <= 2
     w = 4 * VM / wshare
-    if fused:
-        table = {
-            "consensus": w + 8 * V + 4 * M + 4 * M + 4 * M + 4 * tiles + 8 * tiles,  # C, levels, R, rpart, C tile sums
-            "quantise": 8 * M + (4 * M if liquid else 0),
-            "rank": 0.0,
-        }
-    else:
-        table = {
-            "consensus": w + 8 * V + 8 * M,
-            "quantise": 8 * M + 8 * M + (4 * M if liquid else 0),
-            "rank": w + 8 * V + 4 * M + 4 * M + 4 * tiles,
-        }
-    table.update({
+    table = {
+        "consensus": w + 8 * V + 8 * M,
+        "quantise": 8 * M + 8 * M + (4 * M if liquid else 0),
+        "rank": w + 8 * V + 4 * M + 4 * M + 4 * tiles,
         "rowsum": w + (4 * V + 8 * V + 16 * V) / wshare,
         "incentive": 4 * M + 4 * tiles + 4 * M,
         "bonds": (w + 8 * V + 4 * M + (4 * M if colnorm else 0) + (4 * M if liquid else 0)
                   + (4 * VM if hist else 0) + 4 * V * ptiles + 8 * VM / max(chunk, 1)),
         "finalize": 4 * V * ptiles + 4 * V + 4 * V,
-    })
+    }
     return float(table[phase])
 
 
@@ -109,21 +88,15 @@ PHASE_KERNELS = {"rowsum": "k_rowsum", "consensus": "k_consensus_w", "quantise":
 
 
 def kernel_of(phase: str, variant: int, shared: bool = False, V: int = 256, M: int = 4096,
-              N: int = 1) -> str | None:
+              N: int = 1) -> str:
     """The kernel that runs a phase (as rocprofv3 names it) for run outputs:
     the bond scan is k_bonds_elem for Yuma 3/4 (k_bonds_grp for a sweep over
     one shared input trajectory), and for YumaRust / Yuma 1 / Yuma 2 the strip
-    scan k_bonds_cn above 64 validators (k_bonds on 64-miner tiles below);
-    consensus / quantise / rank are k_cons_rank / k_liquid / none on the
-    fused path (fused_cons_rank)."""
+    scan k_bonds_cn above 64 validators (k_bonds on 64-miner tiles below)."""
     if phase == "bonds":
         if variant >= 3:
             return "k_bonds_grp" if shared and N > 1 else "k_bonds_elem"
         return "k_bonds_cn" if V > 64 and M % 4 == 0 else "k_bonds"
-    if fused_cons_rank(variant, V, M, shared, N):
-        fused = {"consensus": "k_cons_rank", "quantise": "k_liquid", "rank": None}
-        if phase in fused:
-            return fused[phase]
     return PHASE_KERNELS[phase]
 
 
@@ -396,19 +369,18 @@ def engine_line(args, variant: int, params: list, W, S, world: int, dist: bool, 
     eff_chunk = chunk if 0 < chunk <= E else E
     launches = -(-E // eff_chunk)  # launches of each phase kernel per step
     wshare = N if shared else 1
-    fused = fused_cons_rank(variant, V, M, shared, N)
     phase_info = {}
     for i, name in enumerate(engine.PHASES):
         kname = kernel_of(name, variant, shared, V, M, N)
-        if phases[i] <= 0 or kname is None:
+        if phases[i] <= 0:
             continue
-        b = phase_bytes(name, V, M, variant, liquid, hist, eff_chunk, wshare, fused) * units
+        b = phase_bytes(name, V, M, variant, liquid, hist, eff_chunk, wshare) * units
         phase_info[name] = {"kernel": kname, "ms": round(float(phases[i]), 4),
                             "GBps": round(b / (phases[i] * 1e-3) / 1e9, 1)}
     dom_name = max(phase_info, key=lambda k: phase_info[k]["ms"])
     dom = engine.PHASES.index(dom_name)
     dom_kernel = kernel_of(dom_name, variant, shared, V, M, N)
-    dom_bytes = phase_bytes(dom_name, V, M, variant, liquid, hist, eff_chunk, wshare, fused) * units / launches
+    dom_bytes = phase_bytes(dom_name, V, M, variant, liquid, hist, eff_chunk, wshare) * units / launches
     dom_ms = float(phases[dom]) / launches
     k_achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
 
@@ -587,17 +559,16 @@ def bench_wide(args, world: int, rank: int, dist: bool) -> dict:
         buf = [0.0] * len(engine.PHASES)
         engine.run(variant, params, W, S, want_hist=hist, workspace=ws, phase_ms=buf)
         liquid = any(p.liquid_mode != engine.LIQUID_OFF for p in params)
-        fused = fused_cons_rank(variant, V, M)
         phases = {}
         for i, name in enumerate(engine.PHASES):
             kname = kernel_of(name, variant, False, V, M)
-            if buf[i] > 0 and kname is not None:
-                b = phase_bytes(name, V, M, variant, liquid, hist, E, 1, fused) * E
+            if buf[i] > 0:
+                b = phase_bytes(name, V, M, variant, liquid, hist, E) * E
                 phases[name] = {"kernel": kname, "ms": round(buf[i], 4),
                                 "GBps": round(b / (buf[i] * 1e-3) / 1e9, 1)}
         dom = max(phases, key=lambda k: phases[k]["ms"])
         dk = kernel_of(dom, variant, False, V, M)
-        db = phase_bytes(dom, V, M, variant, liquid, hist, E, 1, fused) * E
+        db = phase_bytes(dom, V, M, variant, liquid, hist, E) * E
         line["roofline"]["kernel"] = {
             "name": dk, "launches_per_step": 1, "avg_ms": phases[dom]["ms"], "bytes_per_launch": db,
             "achieved": phases[dom]["GBps"], "frac": round(phases[dom]["GBps"] / HBM_PEAK_GBPS, 4),

@@ -40,7 +40,6 @@
 #include <stdlib.h>
 #include <string.h>
 
-#include <type_traits>
 #include <vector>
 
 #include "yuma_hip.h"
@@ -360,11 +359,11 @@ __device__ __forceinline__ void load4_vec(const float* __restrict__ v, int m, in
 constexpr int kWideChunks = 64, kMaxWideChunks = 4096;
 // RN(1 / rs) when div_fast of every weight of the row by rs takes its fast
 // path (|rs| and every nonzero |w| in [2^-60, 2^60]; bmax / bmin1: the row's
-// max |w| and min nonzero |w| - 1 as bit patterns), else NaN: the bond scans
-// then divide without a per-row reciprocal or a per-element guard
-// (k_bonds_elem, k_bonds_grp). k_rowsum stores it per INPUT slice and row as
-// rq4 = {row sum, this, normalised stake, 0}: one 16-byte load per row and
-// epoch.
+// max |w| and min nonzero |w| - 1 as bit patterns), else NaN: the sweep
+// scan then divides without a per-row reciprocal or a per-element guard
+// (k_bonds_grp; the memory-bound scans lost with it, k_bonds_elem). k_rowsum
+// stores it per INPUT slice and row as rq4 = {row sum, this, normalised stake,
+// 0}: one 16-byte load per row and epoch.
 __device__ __forceinline__ bool screen_ok(unsigned bmax, unsigned bmin1) {
   return bmax <= __float_as_uint(0x1p60f) && (bmin1 == 0xFFFFFFFFu || bmin1 + 1u >= __float_as_uint(0x1p-60f));
 }
@@ -372,11 +371,7 @@ __device__ __forceinline__ float fast_row_rcp(float rs, unsigned bmax, unsigned 
   const float ad = fabsf(rs);
   return ad >= 0x1p-60f && ad <= 0x1p60f && screen_ok(bmax, bmin1) ? 1.0f / rs : qnan();
 }
-// a column shard's row (partial row sum): 1 when its own weights pass the
-// screen, else NaN; k_add_eps completes it once the row sum is known
-__device__ __forceinline__ float screen_mark(unsigned bmax, unsigned bmin1) {
-  return screen_ok(bmax, bmin1) ? 1.0f : qnan();
-}
+
 template <bool VEC, bool WIDE = false>
 __global__ __launch_bounds__(256) void k_rowsum(const float* __restrict__ W,
                                                 const float* __restrict__ S, int V, int M,
@@ -451,8 +446,7 @@ __global__ __launch_bounds__(256) void k_rowsum(const float* __restrict__ W,
           bx = max(bx, qb[0][w]);
           bn = min(bn, qb[1][w]);
         }
-        *reinterpret_cast<float2*>(&rq4[wsl * V + rb]) =
-            make_float2(rs, partial ? screen_mark(bx, bn) : fast_row_rcp(rs, bx, bn));
+        *reinterpret_cast<float2*>(&rq4[wsl * V + rb]) = make_float2(rs, fast_row_rcp(rs, bx, bn));
       }
     }
   }
@@ -492,8 +486,7 @@ __global__ __launch_bounds__(256) void k_rowsum(const float* __restrict__ W,
         bmin1 = min(bmin1, (unsigned)__shfl_xor((int)bmin1, o, 64));
       }
       if (lane == 0)
-        *reinterpret_cast<float2*>(&rq4[wsl * V + row]) =
-            make_float2(rs, partial ? screen_mark(bmax, bmin1) : fast_row_rcp(rs, bmax, bmin1));
+        *reinterpret_cast<float2*>(&rq4[wsl * V + row]) = make_float2(rs, fast_row_rcp(rs, bmax, bmin1));
     }
   }
   // the stake normalisation: output slices f = rb, rb + rowblocks, ... of
@@ -1275,283 +1268,6 @@ __global__ __launch_bounds__(256, 4) void k_consensus_w(const float* __restrict_
       if (m + c < M) craw[slice * M + m + c] = (double)hi_k[c] / (double)top;
 }
 
-// ---------------------------------------------------------------------------
-// Consensus, quantisation and rank from ONE read of W (run outputs: no
-// materialised Wn / Wc / T_v, no shared-input consensus classes, not Yuma2,
-// whose rank clips W_prev; yumas.py:192-217, YumaRust :78-106).
-// The rank needs the quantised consensus, i.e. ΣC over EVERY tile of the
-// slice (yumas.py:211), so it cannot run in the tile's consensus block
-// without a per-slice hand-off. k_cons_rank is a persistent grid (G blocks,
-// as many as fit at once, G a multiple of the tiles per slice) walking the
-// (slice, tile) items in slice-major order: block b takes items b, b + G,
-// b + 2G, ..., so a slice's tiles are one round of 64 consecutive blocks.
-// Per item the block runs k_consensus_w's load / normalisation / prerank /
-// search with the tile resident in registers and publishes the tile's C_raw
-// sum (an agent-scope counter per slice; the slice's last tile adds the tile
-// sums in order: csum_canonical's ΣC). The hand-offs follow the guide's
-// sc1 protocol (MI355X_MICROARCH.md, inter-workgroup visibility, first row):
-// payloads stored and loaded sc1 (relaxed agent atomics), the storing wave's
-// vmcnt(0) before a relaxed agent add, relaxed sc1 polls — no L2 write-back
-// or L1 invalidate per item. One round later — while its next
-// item's W is in flight — it quantises its previous tile's columns with that
-// ΣC (k_quantise's formula) and ranks them from the tile still in registers
-// (two register sets, alternating), in k_rank_s's summation order. So the
-// slice's other blocks have a full round to publish; W is read once for
-// consensus and rank. Every wait only looks at items of the previous round
-// (all resident), and a bounded spin sets *err instead of hanging.
-// Liquid alpha (quantiles of all levels) runs after it in k_liquid.
-// ---------------------------------------------------------------------------
-struct ConsRankArgs {
-  const float* W;
-  const float* rsd;
-  const float* sn;
-  const int* sx;
-  const yuma_params_t* prm;
-  float* P;        // prerank (optional)
-  float* C;        // quantised consensus [slice][M]
-  int* qlev;       // its integer levels
-  float* R;        // rank
-  float* rpart;    // rank tile sums [slice][tile]
-  double* ctile;   // C_raw tile sums [slice - slice0][tile] (fp32 values, YumaRust fp64)
-  int* cnt;        // per slice: tiles published, +1 once ΣC is stored (zeroed before the launch)
-  float* sumc_f;   // ΣC per slice (chunk-relative, as k_liquid reads it)
-  double* sumc_d;
-  int* err;        // a wait ran out (never expected: every block is resident)
-  long long slice0, nslices;
-  int N, V, M, tiles;
-};
-
-constexpr int kConsRankSpin = 1 << 20;
-
-template <bool RUST>
-__global__ __launch_bounds__(256, 2) void k_cons_rank(ConsRankArgs A) {
-  constexpr int R = 16, NR = 16 * R, PL = NR / 64;
-  typedef typename std::conditional<RUST, double, float>::type T;
-  __shared__ __attribute__((aligned(16))) unsigned hb[kHistWords];
-  __shared__ __attribute__((aligned(16))) float rl[4][48 * R];
-  __shared__ T tred[2][4];      // C_raw wave sums of the item being published
-  __shared__ float rred[2][4];  // rank wave sums of the item being ranked
-  __shared__ T cst[512];        // a slice's C_raw tile sums (its last block; tiles <= 512)
-  const WLay L = wlay();
-  const int V = A.V, M = A.M, tiles = A.tiles, N = A.N;
-  const long long items = A.nslices * tiles;
-  const long long G = gridDim.x;
-  const long long VM = (long long)V * M;
-
-  // the resident tile: normalised weights and the consensus grid index of
-  // this lane's 4 columns; the rows' sums / stakes / reciprocals in rl
-  float X[R][4];
-  int hX[4];
-  int par = 0;
-  for (long long it = blockIdx.x;; it += G, par ^= 1) {
-    const bool cur = it < items;  // block-uniform
-    const long long prv = it - G;
-    // --- rank of the previous round's item (its tile still in X, stakes in rl)
-    if (prv >= 0 && prv < items) {
-      const long long ps = A.slice0 + prv / tiles, pr = prv / tiles;
-      const int pt = (int)(prv % tiles);
-      const int pm = pt * kTileM + L.wave * 16 + L.cq * 4;
-      const int pn = (int)(ps % N);
-      const int iters = A.prm[pn].bisect_iters;
-      // ONE lane polls (sc1 loads); the block's other waves load ΣC after the
-      // barrier that lane's wave joins once its poll matched
-      if (threadIdx.x == 0 && __hip_atomic_load(A.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
-        for (int spin = 0; __hip_atomic_load(A.cnt + pr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <= tiles;) {
-          __builtin_amdgcn_s_sleep(8);
-          if (++spin > kConsRankSpin) {  // never expected; later waits are skipped
-            __hip_atomic_store(A.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            break;
-          }
-        }
-      }
-      lds_barrier();
-      float Cq[4];
-      int lev[4];
-      const double top = (double)(1 << iters);
-      if constexpr (RUST) {
-        const double sd = __hip_atomic_load(A.sumc_d + pr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll
-        for (int c = 0; c < 4; ++c) lev[c] = (int)((double)hX[c] / top / sd * 65535.0);
-      } else {
-        const float sf = __hip_atomic_load(A.sumc_f + pr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll
-        for (int c = 0; c < 4; ++c) lev[c] = (int)((float)((double)hX[c] / top) / sf * 65535.0f);
-      }
-#pragma unroll
-      for (int c = 0; c < 4; ++c) Cq[c] = level_value(lev[c]);
-      const LdsRows s{&rl[0][0], L.wave * 48 * R + 16 * R + L.rg};
-      float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-      for (int i = 0; i < R; ++i) {
-        const float si = s[i];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) acc[c] = acc[c] + si * vmin(X[i][c], Cq[c]);
-      }
-#pragma unroll
-      for (int c = 0; c < 4; ++c) acc[c] = wsum16(acc[c]);
-      if (L.rg == 0)
-#pragma unroll
-        for (int c = 0; c < 4; ++c)
-          if (pm + c < M) {
-            A.C[ps * M + pm + c] = Cq[c];
-            A.qlev[ps * M + pm + c] = lev[c];
-            A.R[ps * M + pm + c] = acc[c];
-          }
-      // the tile sum as the 64-lane butterfly over the tile's miners
-      float q = (acc[0] + acc[1]) + (acc[2] + acc[3]);
-      q = q + __shfl_xor(q, 16, 64);
-      q = q + __shfl_xor(q, 32, 64);
-      if (L.lane == 0) rred[par][L.wave] = q;
-      lds_barrier();
-      if (threadIdx.x == 0)
-        A.rpart[ps * tiles + pt] = (rred[par][0] + rred[par][1]) + (rred[par][2] + rred[par][3]);
-    }
-    if (!cur) break;
-    long long slice = 0;
-    int tile = 0, m = 0;
-    float dv[PL], sv[PL];
-    bool full = true, allfull = true;
-    {
-      slice = A.slice0 + it / tiles;
-      tile = (int)(it % tiles);
-      m = tile * kTileM + L.wave * 16 + L.cq * 4;
-      const float* Ws = A.W + slice * VM;
-      const float* rsd_s = A.rsd + slice * V;
-      const float* sn_s = A.sn + slice * V;
-#pragma unroll
-      for (int k = 0; k < PL; ++k) {
-        const int jj = min(L.lane + 64 * k, V - 1);
-        dv[k] = rsd_s[jj];
-        sv[k] = sn_s[jj];
-      }
-      full = L.rg + 16 * (R - 1) < V && m + 3 < M;
-      allfull = __all(full);
-      if (allfull) {
-        unsigned o0 = (unsigned)L.rg * (unsigned)M + (unsigned)m, st = 16u * (unsigned)M;
-        // opaque per item: the compiler would otherwise hoist the 16 row
-        // offsets out of the persistent loop (16 more live registers)
-        asm volatile("" : "+v"(o0), "+s"(st));
-#pragma unroll
-        for (int i = 0; i < R; ++i) {
-          const float4 t = *reinterpret_cast<const float4*>(Ws + (o0 + (unsigned)i * st));
-          X[i][0] = t.x;
-          X[i][1] = t.y;
-          X[i][2] = t.z;
-          X[i][3] = t.w;
-        }
-      } else {
-#pragma unroll
-        for (int i = 0; i < R; ++i) load4c<true>(Ws, L.rg + 16 * i, V, m, M, X[i]);
-      }
-    }
-    // --- consensus of this round's item (k_consensus_w on a resident tile)
-    {
-      float* rlw = &rl[L.wave][0];
-      float amax = 0.0f, dmin = INFINITY;
-#pragma unroll
-      for (int k = 0; k < PL; ++k) {
-        const int j = L.lane + 64 * k;
-        amax = fmaxf(amax, fabsf(dv[k]));
-        dmin = fminf(dmin, fabsf(dv[k]));
-        rlw[j] = dv[k];
-        rlw[NR + j] = j < V ? sv[k] : 0.0f;
-        rlw[2 * NR + j] = 1.0f / dv[k];
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      typedef float f2 __attribute__((ext_vector_type(2)));
-      unsigned ymin = 0xFFFFFFFFu;
-#pragma unroll
-      for (int i = 0; i < R; ++i) {
-        const float d = rlw[L.rg + 16 * i];
-        const float r = rlw[2 * NR + L.rg + 16 * i];
-        const f2 r2 = {r, r}, nd2 = {-d, -d};
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const f2 a2 = {X[i][2 * h], X[i][2 * h + 1]};
-#pragma unroll
-          for (int c = 0; c < 2; ++c) {
-            amax = fmaxf(amax, fabsf(a2[c]));
-            const unsigned y = (__float_as_uint(a2[c]) << 1) - 1u;
-            ymin = y < ymin ? y : ymin;
-          }
-          const f2 q = a2 * r2;
-          const f2 e = __builtin_elementwise_fma(nd2, q, a2);
-          const f2 q1 = __builtin_elementwise_fma(e, r2, q);
-          X[i][2 * h] = q1[0];
-          X[i][2 * h + 1] = q1[1];
-        }
-      }
-      const bool slow = !(dmin >= 0x1p-60f && amax <= 0x1p60f &&
-                          (ymin == 0xFFFFFFFFu || ymin + 1u >= (__float_as_uint(0x1p-60f) << 1)));
-      if (__any(slow)) {  // rare: some operand outside the fast-division guard
-        const float* Ws = A.W + slice * VM;
-#pragma unroll
-        for (int i = 0; i < R; ++i) {
-          load4c<true>(Ws, L.rg + 16 * i, V, m, M, X[i]);
-          const float d = rlw[L.rg + 16 * i];
-#pragma unroll
-          for (int c = 0; c < 4; ++c) X[i][c] = X[i][c] / d;
-        }
-      }
-      if (!allfull) {
-#pragma unroll
-        for (int i = 0; i < R; ++i) mask4(L.rg + 16 * i, V, m, M, X[i]);
-      }
-    }
-    const LdsRows s{&rl[0][0], L.wave * 48 * R + 16 * R + L.rg};
-    const int n = (int)(slice % N);
-    if (A.P != nullptr) prerank_store<R>(X, s, L, m, M, A.P + slice * M);
-    const yuma_params_t& p = A.prm[n];
-    const bool hist_ok = !(p.flags & YUMA_FLAG_NO_HIST);
-    consensus_search<R, 16>(X, s, p.kappa, p.bisect_iters, hist_ok ? A.sx[slice] : -1,
-                            hb + L.wave * 16 * kHS, L.lane, L.cq, L.rg, hX);
-    // --- publish the tile's C_raw sum (csum_canonical's in-tile butterfly)
-    {
-      const double top = (double)(1 << p.bisect_iters);
-      T v[4];
-#pragma unroll
-      for (int c = 0; c < 4; ++c) v[c] = m + c < M ? (T)((double)hX[c] / top) : (T)0;
-      T q = (v[0] + v[1]) + (v[2] + v[3]);
-      q = q + __shfl_xor(q, 16, 64);
-      q = q + __shfl_xor(q, 32, 64);
-      if (L.lane == 0) tred[par][L.wave] = q;
-      lds_barrier();
-      if (L.wave == 0) {
-        const long long sr = slice - A.slice0;
-        int old = 0;
-        if (L.lane == 0) {
-          const T ts = (tred[par][0] + tred[par][1]) + (tred[par][2] + tred[par][3]);
-          __hip_atomic_store(A.ctile + sr * tiles + tile, (double)ts, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the sc1 store has left before the add
-          old = __hip_atomic_fetch_add(A.cnt + sr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        old = __shfl(old, 0, 64);
-        if (old == tiles - 1) {  // the slice's last tile: ΣC, tiles in order
-          // every tile sum in flight at once (sc1 loads, lane k: tiles k, k + 64, ...),
-          // parked in LDS, added in tile order by one lane
-          for (int k = L.lane; k < tiles; k += 64)
-            cst[k] = (T)__hip_atomic_load(A.ctile + sr * tiles + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-          __builtin_amdgcn_wave_barrier();
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-          if (L.lane == 0) {
-            T tot = (T)0;
-            for (int k = 0; k < tiles; ++k) tot = tot + cst[k];
-            if constexpr (RUST)
-              __hip_atomic_store(A.sumc_d + sr, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            else
-              __hip_atomic_store(A.sumc_f + sr, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __hip_atomic_fetch_add(A.cnt + sr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          }
-        }
-      }
-    }
-  }
-}
-
 // Clip + rank (yumas.py:214-217; Yuma2 clips W_prev :328), wave-owned columns.
 // rpart[slice][tile] = sum over the tile's 64 miners (wave sums, waves in order).
 template <int R, bool VEC, bool YUMA2, bool FULL>
@@ -1673,11 +1389,8 @@ __global__ __launch_bounds__(256) void k_rank_w(
 // across rows, so the block takes the bond kernel's wide layout (a wave
 // instruction moves 4 rows x 256 contiguous bytes instead of 16 x 64) and
 // streams its rows in batches of 8 loads per lane. Order: rows g, g+16, ...
-// sequentially per lane, then the 16 row groups as a pairwise tree (the 4 row
-// groups of a wave by xor 16, 32; the 4 waves as (w0 + w1) + (w2 + w3)) —
-// the order of the DPP row tree wsum16 over rows rg + 16 i, so k_cons_rank
-// (rank from the consensus kernel's resident tile) gives the same bits. The
-// tile sum is the 64-lane butterfly over the tile's miners. YUMA2 clips the previous epoch's normalised weights
+// sequentially per lane, then the 4 row groups of a wave (xor 16, 32), then
+// the 4 waves in order. YUMA2 clips the previous epoch's normalised weights
 // instead (yumas.py:299-300, 328-331: W_prev, at the first epoch the caller's
 // W_prev or W itself) with this epoch's stakes: the previous slice divided by
 // its own row sums — only W_prev is read, not W.
@@ -1760,7 +1473,9 @@ __global__ __launch_bounds__(256, 1) void k_rank_s(const float* __restrict__ W,
   if (L.wave == 0) {
     // lane l: miner tile*64 + l
     const float* rf = reinterpret_cast<const float*>(&red[0][0]);
-    const float r = (rf[L.lane] + rf[64 + L.lane]) + (rf[128 + L.lane] + rf[192 + L.lane]);
+    float r = rf[L.lane];
+#pragma unroll
+    for (int w = 1; w < 4; ++w) r = r + rf[w * 64 + L.lane];
     const int mg = tile * kTileM + L.lane;
     if (mg < M) Rout[slice * M + mg] = r;
     float t = mg < M ? r : 0.0f;
@@ -1794,40 +1509,6 @@ __device__ double block_sum_d(double x, double* red) {
   double t = red[0];
   for (int w = 1; w < NW; ++w) t = t + red[w];
   return t;
-}
-
-// ΣC_raw in the engine's canonical order (yumas.py:211 `C.sum()`, YumaRust
-// :97 in fp64): each 64-miner tile summed as the 64-lane butterfly over its
-// columns (padding 0), the tile sums added in tile order. k_quantise, k_csum
-// (per shard, then the shards in order) and k_cons_rank (each block its tile;
-// the last block of a slice adds the tiles) give the same bits. T = float
-// (the fp32 sum of (float) C_raw) or double (YumaRust).
-constexpr int kCsumStage = 1024;
-template <typename T, int NT>
-__device__ T csum_canonical(const double* __restrict__ cr, int M, T* stage /*[kCsumStage + 1]*/) {
-  constexpr int NW = NT / 64;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int tiles = (M + 63) / 64;
-  T acc = (T)0;
-  for (int k0 = 0; k0 < tiles; k0 += kCsumStage) {
-    const int nk = min(tiles - k0, kCsumStage);
-    for (int k = wave; k < nk; k += NW) {
-      const int m = (k0 + k) * 64 + lane;
-      T v = m < M ? (T)cr[m] : (T)0;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) v = v + __shfl_xor(v, o, 64);
-      if (lane == 0) stage[k] = v;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0)
-      for (int k = 0; k < nk; ++k) acc = acc + stage[k];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) stage[kCsumStage] = acc;
-  __syncthreads();
-  const T tot = stage[kCsumStage];
-  __syncthreads();
-  return tot;
 }
 
 // high-byte histogram of the levels (four loads in flight per thread)
@@ -1925,7 +1606,8 @@ __global__ __launch_bounds__(NT) void k_quantise(const double* __restrict__ craw
                                                  const float* __restrict__ ext_sumf,
                                                  const double* __restrict__ ext_sumd,
                                                  int no_liquid, const int* __restrict__ crep) {
-  __shared__ double stage[kCsumStage + 1];
+  __shared__ float redf[NT / 64];
+  __shared__ double redd[NT / 64];
   __shared__ int hist1[256], hist2[256], bc[4];
   const long long slice = slice0 + blockIdx.x;
   const yuma_params_t& p = prm[slice % N];
@@ -1944,10 +1626,30 @@ __global__ __launch_bounds__(NT) void k_quantise(const double* __restrict__ craw
       sumf = ext_sumf[slice];
     }
   } else if (variant == YUMA_VARIANT_RUST) {
-    sumd = csum_canonical<double, NT>(cr, M, stage);
+    double acc = 0.0;
+    int m = threadIdx.x;
+    for (; m + 3 * NT < M; m += 4 * NT) {  // loads in flight, same summation order
+      const double x0 = cr[m], x1 = cr[m + NT], x2 = cr[m + 2 * NT], x3 = cr[m + 3 * NT];
+      acc = acc + x0;
+      acc = acc + x1;
+      acc = acc + x2;
+      acc = acc + x3;
+    }
+    for (; m < M; m += NT) acc = acc + cr[m];
+    sumd = block_sum_d<NT>(acc, redd);
     sumf = (float)sumd;
   } else {
-    sumf = csum_canonical<float, NT>(cr, M, reinterpret_cast<float*>(stage));
+    float acc = 0.0f;
+    int m = threadIdx.x;
+    for (; m + 3 * NT < M; m += 4 * NT) {  // loads in flight, same summation order
+      const double x0 = cr[m], x1 = cr[m + NT], x2 = cr[m + 2 * NT], x3 = cr[m + 3 * NT];
+      acc = acc + (float)x0;
+      acc = acc + (float)x1;
+      acc = acc + (float)x2;
+      acc = acc + (float)x3;
+    }
+    for (; m < M; m += NT) acc = acc + (float)cr[m];
+    sumf = block_sum<NT>(acc, redf);
   }
   for (int m = threadIdx.x; m < M; m += NT) {
     int lev;
@@ -2851,23 +2553,15 @@ __global__ __launch_bounds__(BS, 1) void k_bonds_elem(BondArgs A) {
     }
   }
 
-  float rw[P][R][4], rd[P][R], rq[P][R], rsn[P][R], ri[P][4], rba[P][4];
+  float rw[P][R][4], rd[P][R], rsn[P][R], ri[P][4], rba[P][4];
   auto fetch = [&](int k, int t) {
     const long long slice = (long long)t * N + n;
-    const long long wsl = A.wsh ? (long long)t : slice;
 #pragma unroll
     for (int i = 0; i < R; ++i) {
       const int rr = min(row0 + G * i, V - 1);
-      load4c<VEC>(A.W + wsl * VM, rr, V, m, M, rw[k][i]);
-      if (NT) {  // the history scans: row sums and stakes, reciprocal per row
-        rd[k][i] = A.rsd[slice * V + rr];
-        rsn[k][i] = A.sn[slice * V + rr];
-      } else {
-        const float4 q = A.rq4[wsl * V + rr];  // {row sum, reciprocal or NaN, stake, 0}
-        rd[k][i] = q.x;
-        rq[k][i] = q.y;
-        rsn[k][i] = q.z;
-      }
+      load4c<VEC>(A.W + (A.wsh ? (long long)t : slice) * VM, rr, V, m, M, rw[k][i]);
+      rd[k][i] = A.rsd[slice * V + rr];
+      rsn[k][i] = A.sn[slice * V + rr];
     }
     // columns >= M never reach an output
     if (VECI) {
@@ -2923,32 +2617,16 @@ __global__ __launch_bounds__(BS, 1) void k_bonds_elem(BondArgs A) {
         constexpr bool SHORT = !(VARIANT == YUMA_VARIANT_YUMA4 && NT);
         auto mn = [](float a, float b) { return SHORT ? vmin(a, b) : tmin(a, b); };
         auto mx = [](float a, float b) { return SHORT ? vmax(a, b) : tmax(a, b); };
-        // div_fast(_nz)'s result from k_rowsum's screened reciprocal when
-        // every row of the wave passed the screen, else IEEE (same values
-        // up to the sign of a zero, which SHORT forms cannot show). The
-        // history scans keep the per-row reciprocal and guard: with the
-        // stored reciprocal the c2 wide scan ran 1.58 -> 1.70 ms (same box).
+        // (k_rowsum's screened reciprocal instead of the per-row one and the
+        // per-element guard: c2 wide history scan 1.58 -> 1.70 ms, c4 1.63 ->
+        // 1.73, same box; kept only in the issue-bound sweep scan k_bonds_grp)
         float wn[4];
-        if (NT) {
-          const RowDiv rdv = row_div(rd[k][i]);
-          bool slow = false;
+        const RowDiv rdv = row_div(rd[k][i]);
+        bool slow = false;
 #pragma unroll
-          for (int c = 0; c < 4; ++c)
-            wn[c] = SHORT ? div_fast_nz(rw[k][i][c], rdv, slow) : div_fast(rw[k][i][c], rdv, slow);
-          if (__any(slow)) {
-#pragma unroll
-            for (int c = 0; c < 4; ++c) wn[c] = rw[k][i][c] / rd[k][i];
-          }
-        } else if (__all(rq[k][i] == rq[k][i])) {
-#pragma unroll
-          for (int c = 0; c < 4; ++c) {
-            const float a = rw[k][i][c];
-            const float q = a * rq[k][i];
-            const float e = fmaf(-rd[k][i], q, a);
-            const float q1 = fmaf(e, rq[k][i], q);
-            wn[c] = SHORT ? q1 : (a == 0.0f ? q : q1);
-          }
-        } else {
+        for (int c = 0; c < 4; ++c)
+          wn[c] = SHORT ? div_fast_nz(rw[k][i][c], rdv, slow) : div_fast(rw[k][i][c], rdv, slow);
+        if (__any(slow)) {
 #pragma unroll
           for (int c = 0; c < 4; ++c) wn[c] = rw[k][i][c] / rd[k][i];
         }
@@ -3419,32 +3097,28 @@ __global__ __launch_bounds__(256) void k_finalize(const float* __restrict__ dpar
 // reduced values. Each partial is a fixed-order sum over this shard's columns.
 // ---------------------------------------------------------------------------
 // rsd = (sum of the shards' row sums) + 1e-6 (yumas.py:186)
-// and rq4 = {row sum, RN(1 / row sum) or NaN, stake, 0} from stage 1's screen mark
 __global__ __launch_bounds__(256) void k_add_eps(const float* __restrict__ rowsum, long long n,
-                                                 float* __restrict__ rsd, float4* __restrict__ rq4) {
-  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
-    const float rs = rowsum[i] + 1e-6f;
-    rsd[i] = rs;
-    float4 q = rq4[i];
-    const float ad = fabsf(rs);
-    q.x = rs;
-    q.y = q.y == q.y && ad >= 0x1p-60f && ad <= 0x1p60f ? 1.0f / rs : qnan();
-    rq4[i] = q;
-  }
+                                                 float* __restrict__ rsd) {
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256)
+    rsd[i] = rowsum[i] + 1e-6f;
 }
-// per slice: sum over this shard's columns of C_raw (fp32; YumaRust fp64),
-// in the canonical order over the shard's tiles (csum_canonical)
+// per slice: sum over this shard's columns of C_raw (fp32; YumaRust fp64)
 __global__ __launch_bounds__(256) void k_csum(const double* __restrict__ craw, int rust, int M,
                                               float* __restrict__ csum_f,
                                               double* __restrict__ csum_d) {
-  __shared__ double stage[kCsumStage + 1];
+  __shared__ float redf[4];
+  __shared__ double redd[4];
   const long long slice = blockIdx.x;
   const double* cr = craw + slice * M;
   if (rust) {
-    const double acc = csum_canonical<double, 256>(cr, M, stage);
+    double acc = 0.0;
+    for (int m = threadIdx.x; m < M; m += 256) acc = acc + cr[m];
+    acc = block_sum_d<256>(acc, redd);
     if (threadIdx.x == 0) csum_d[slice] = acc;
   } else {
-    const float acc = csum_canonical<float, 256>(cr, M, reinterpret_cast<float*>(stage));
+    float acc = 0.0f;
+    for (int m = threadIdx.x; m < M; m += 256) acc = acc + (float)cr[m];
+    acc = block_sum<256>(acc, redf);
     if (threadIdx.x == 0) csum_f[slice] = acc;
   }
 }
@@ -3548,9 +3222,6 @@ struct Workspace {
   float* sumc_f;
   double* sumc_d;
   int* crep;  // per scenario: consensus class representative (k_classes)
-  double* ctile;  // k_cons_rank: C_raw tile sums [slice][tile]
-  int* cnt;       // k_cons_rank: per-slice publish counters
-  int* err;       // k_cons_rank: a wait ran out
   size_t bytes;
 };
 
@@ -3590,9 +3261,6 @@ Workspace carve(char* base, int variant, int N, int E, int V, int M, int full) {
   w.sumc_f = (float*)take(S * 4);
   w.sumc_d = (double*)take(S * 8);
   w.crep = (int*)take((size_t)N * 4);
-  w.ctile = (double*)take(S * tiles * 8);
-  w.cnt = (int*)take(S * 4);
-  w.err = (int*)take(4);
   w.bytes = off;
   return w;
 }
@@ -3855,21 +3523,6 @@ struct PhaseTimer {
   }
 };
 
-// Persistent grid of k_cons_rank: as many blocks as fit on the device at
-// once, rounded down to whole slices of tiles (so a slice's tiles are one
-// round); 0 when a slice has more tiles than that (the multi-pass path).
-long long cons_rank_grid(bool rust, int tiles) {
-  int dev = 0, cus = 0, nb = 0;
-  if (hipGetDevice(&dev) != hipSuccess ||
-      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-    return 0;
-  const hipError_t e = rust ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, yk::k_cons_rank<true>, 256, 0)
-                            : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, yk::k_cons_rank<false>, 256, 0);
-  if (e != hipSuccess || nb < 1) return 0;
-  const long long cap = (long long)nb * cus;
-  return cap >= tiles && tiles <= 512 ? cap / tiles * tiles : 0;  // 512: k_cons_rank's cst
-}
-
 int run_impl(int variant, const yuma_params_t* prm, int N, int E, int V, int M, const float* W,
              const float* S, const float* B_init, const float* Wprev_init,
              const yuma_outputs_t* out, void* workspace, size_t ws_bytes, int chunk,
@@ -3925,12 +3578,6 @@ int run_impl(int variant, const yuma_params_t* prm, int N, int E, int V, int M, 
   const bool rank_stream = out->Wn == nullptr && out->Wc == nullptr && ws.tvc == nullptr &&
                            variant != YUMA_VARIANT_YUMA2;  // Yuma2's W_prev: rank per scenario
   const int* rcrep = rank_stream ? crep : nullptr;
-  // consensus + quantisation + rank from one read of W (k_cons_rank): run
-  // outputs of 65-256 validators, whole 64-miner tiles, no consensus classes
-  const bool rust = variant == YUMA_VARIANT_RUST;
-  long long cr_grid = 0;
-  if (vec && rank_stream && crep == nullptr && rc == RC_256_16 && M % yk::kTileM == 0)
-    cr_grid = cons_rank_grid(rust, tiles);
 
   PhaseTimer tm{};
   tm.ms = phase_ms;
@@ -3961,34 +3608,17 @@ int run_impl(int variant, const yuma_params_t* prm, int N, int E, int V, int M, 
         YK_LAUNCH(yk::k_rowsum<false>, rs_in * rowblocks4, 256, st, W, S, V, M, rs_s0,
                   rowblocks4, ws.rsd, ws.sn, 0, ws.sx, fan, ws.rq4);
       tm.mark(YUMA_PHASE_CONSENSUS);
-      if (cr_grid > 0) {
-        (void)hipMemsetAsync(ws.cnt, 0, (size_t)ns * 4, st);
-        (void)hipMemsetAsync(ws.err, 0, 4, st);
-        yk::ConsRankArgs CA{W, ws.rsd, ws.sn, ws.sx, prm, out->P, C, ws.qlev, Rr, ws.rpart, ws.ctile,
-                            ws.cnt, ws.sumc_f, ws.sumc_d, ws.err, s0, ns, N, V, M, tiles};
-        const long long g = cr_grid < ns * tiles ? cr_grid : ns * tiles;
-        if (rust)
-          YK_LAUNCH(yk::k_cons_rank<true>, g, 256, st, CA);
-        else
-          YK_LAUNCH(yk::k_cons_rank<false>, g, 256, st, CA);
-        tm.mark(YUMA_PHASE_QUANTISE);  // liquid alpha: quantiles of the levels
-        YK_LAUNCH(yk::k_liquid<256>, ns, 256, st, prm, N, M, s0, C, ws.qlev, M, ba_buf, ws.scal,
-                  ws.sumc_f, ws.sumc_d, rust ? 1 : 0);
-      } else if (vec)
+      if (vec)
         launch_consensus<true>(rc, ns * tiles, st, W, ws.rsd, ws.sn, ws.sx, prm, N, V, M, s0, tiles,
                                ws.craw, out->P, wsh, crep);
       else
         launch_consensus<false>(rc, ns * tiles, st, W, ws.rsd, ws.sn, ws.sx, prm, N, V, M, s0,
                                 tiles, ws.craw, out->P, wsh, crep);
-      if (cr_grid == 0) {
-        tm.mark(YUMA_PHASE_QUANTISE);
-        YK_LAUNCH(yk::k_quantise<256>, ns, 256, st, ws.craw, prm, variant, N, M, s0, C, ws.qlev,
-                  ba_buf, ws.scal, nullptr, nullptr, 0, crep);
-      }
+      tm.mark(YUMA_PHASE_QUANTISE);
+      YK_LAUNCH(yk::k_quantise<256>, ns, 256, st, ws.craw, prm, variant, N, M, s0, C, ws.qlev,
+                ba_buf, ws.scal, nullptr, nullptr, 0, crep);
       tm.mark(YUMA_PHASE_RANK);
-      if (cr_grid > 0) {
-        // ranked by k_cons_rank
-      } else if (vec)
+      if (vec)
         launch_rank<true>(rc, ns * tiles, st, W, ws.rsd, ws.sn, C, Wprev_init,
                           variant == YUMA_VARIANT_YUMA2, N, V, M, s0, tiles, Rr, ws.rpart, out->Wn,
                           out->Wc, ws.tvc, ws.tvn, wsh, rcrep);
@@ -4107,10 +3737,10 @@ int shard_stage_impl(int stage, int variant, const yuma_params_t* prm, int N, in
       const int rb4 = (V + 3) / 4;
       if (vec)
         YK_LAUNCH(yk::k_rowsum<true>, ns * rb4, 256, st, W, S, V, M, 0LL, rb4, io->rowsum_part,
-                  ws.sn, 1, ws.sx, 1, ws.rq4);
+                  ws.sn, 1, ws.sx, 1, (float4*)nullptr);
       else
         YK_LAUNCH(yk::k_rowsum<false>, ns * rb4, 256, st, W, S, V, M, 0LL, rb4, io->rowsum_part,
-                  ws.sn, 1, ws.sx, 1, ws.rq4);
+                  ws.sn, 1, ws.sx, 1, (float4*)nullptr);
       break;
     }
     case 2: {
@@ -4118,7 +3748,7 @@ int shard_stage_impl(int stage, int variant, const yuma_params_t* prm, int N, in
         return fail(YUMA_EINVAL, "stage 2 needs io->rowsum and io->csum_part%s", rust ? "_d" : "");
       long long nb = (ns * V + 255) / 256;
       if (nb > 4096) nb = 4096;
-      YK_LAUNCH(yk::k_add_eps, nb, 256, st, io->rowsum, ns * V, ws.rsd, ws.rq4);
+      YK_LAUNCH(yk::k_add_eps, nb, 256, st, io->rowsum, ns * V, ws.rsd);
       if (vec)
         launch_consensus<true>(rc, ns * tiles, st, W, ws.rsd, ws.sn, ws.sx, prm, N, V, M, 0LL, tiles,
                                ws.craw, out->P, 0, nullptr);
@@ -4175,7 +3805,6 @@ int shard_stage_impl(int stage, int variant, const yuma_params_t* prm, int N, in
       A.Wb_out = out->Wb;
       A.Binst_out = out->B_inst;
       A.dpart = ws.dpart;
-      A.rq4 = ws.rq4;
       A.N = N;
       A.V = V;
       A.M = M;
