@@ -64,8 +64,9 @@ def main():
     ap.add_argument("--M", type=int, default=4096)
     ap.add_argument("--version", default="Yuma 3 (Rhef)")
     ap.add_argument("--history", action="store_true")
-    ap.add_argument("--out", default=os.path.join(os.path.dirname(__file__), "..", "profiles", "r03",
+    ap.add_argument("--out", default=os.path.join(os.path.dirname(__file__), "..", "profiles", "r04",
                                                   "pmc_traffic.json"))
+    ap.add_argument("--commit", default=None, help="git commit of the library the passes ran (ADVICE r3)")
     ap.add_argument("--launches", type=int, default=1, help="launches of each kernel per bench step")
     a = ap.parse_args()
     fetch = counters(a.fetch_dir, "FETCH_SIZE")
@@ -90,6 +91,7 @@ def main():
         "workload": {"V": a.V, "M": a.M, "epochs": a.epochs, "scenarios_per_gpu": a.scenarios,
                      "version": a.version, "bond_history": bool(a.history)},
         "correction": "FETCH_SIZE x2 (gfx950 wide-read half count), KiB -> bytes; WRITE_SIZE as is",
+        "commit": a.commit,
         "step_hbm_bytes": sum(v["hbm_bytes_per_launch"] for v in kernels.values()) * a.launches,
         "kernels": kernels,
     }
