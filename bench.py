@@ -24,7 +24,7 @@ Prints ONE JSON line (rank 0) with the driver's fields plus
                 BYTES(V,M) (the fp32 epoch-step contract, 12,617,728 B at
                 256 x 4096), frac = achieved / 8 TB/s; traffic = the rocprofv3
                 FETCH_SIZE + WRITE_SIZE bytes of one step (committed PMC passes of
-                this exact workload, profiles/r03/pmc_traffic.json), and
+                this exact workload, profiles/r04/pmc_traffic.json), and
                 roofline.kernel = the dominant kernel (k_bonds_elem at c2):
                 algorithmic bytes per launch / its HIP-event launch time;
   cpu_baseline  the torch-CPU restatement of the epoch (oracle/torch_cpu.py,
@@ -100,7 +100,24 @@ def kernel_of(phase: str, variant: int, shared: bool = False, V: int = 256, M: i
     return PHASE_KERNELS[phase]
 
 
-TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r03", "pmc_traffic.json")
+TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r04", "pmc_traffic.json")
+SQ_JSON = os.path.join(ROOT, "profiles", "r04", "sq_valu.json")
+VALU_PEAK_GINST = 1024 * 2.4 / 2  # G wave64 VALU instructions/s: 1024 SIMDs, 2 cycles each, 2.4 GHz
+
+
+def load_sq(key: dict) -> dict | None:
+    """Per-kernel SQ counts per launch (SQ_INSTS_VALU, ...) of the committed SQ
+    pass of this exact workload (tools/sq_summary.py), or None."""
+    try:
+        with open(SQ_JSON) as f:
+            records = json.load(f)
+    except (OSError, ValueError):
+        return None
+    for rec in records:
+        wl = rec.get("workload", {})
+        if all(wl.get(k) == v for k, v in key.items()):
+            return {k: dict(v["counters"], commit=rec.get("commit")) for k, v in rec["kernels"].items()}
+    return None
 
 
 def load_traffic(key: dict) -> dict | None:
@@ -416,23 +433,34 @@ def engine_line(args, variant: int, params: list, W, S, world: int, dist: bool, 
             "kernel": kernel,
         }
     else:
-        # one shared input trajectory: the contract's per-scenario W read
-        # never happens, so the roofline is the MEASURED HBM traffic of a step
-        # (PMC) over its time; the contract-equivalent rate is reported apart
+        # one shared input trajectory: the sweep scan re-reads W from the
+        # caches and is bound by VALU issue, not HBM: the
+        # roofline is the dominant kernel's VALU issue rate — its committed
+        # SQ_INSTS_VALU per launch (SQ pass of this exact workload) over its
+        # live HIP-event time — against the issue peak (1024 SIMDs, a wave64
+        # VALU instruction every 2 cycles at 2.4 GHz, MI355X_MICROARCH.md).
+        # The PMC bytes beyond L2 are reported apart; they are not an HBM
+        # fraction (Infinity-Cache hits count as fetched).
         classes = consensus_classes(params)
         step_s = elapsed / args.steps
-        achieved = None if traffic is None else traffic / step_s / 1e9
+        sq = load_sq(key)
+        valu = None if sq is None or dom_kernel not in sq else sq[dom_kernel]
+        ach = None if valu is None else valu["SQ_INSTS_VALU"] / (dom_ms * 1e-3) / 1e9
         line["roofline"] = {
-            "bound": "hbm",
-            "achieved": None if achieved is None else round(achieved, 1),
-            "peak": HBM_PEAK_GBPS,
-            "unit": "GB/s",
-            "frac": None if achieved is None else round(achieved / HBM_PEAK_GBPS, 4),
-            "traffic": traffic,
-            "definition": ("measured bytes beyond L2 of one step (rocprofv3 FETCH_SIZE + WRITE_SIZE, "
-                           f"{os.path.relpath(TRAFFIC_JSON, ROOT)}; Infinity-Cache hits count as fetched) / the step "
-                           "time / 8 TB/s; the kernel record counts W once per input epoch for all scenarios (each "
-                           "input read once)"),
+            "bound": "valu",
+            "achieved": None if ach is None else round(ach, 2),
+            "peak": VALU_PEAK_GINST,
+            "unit": "G VALU wave-instructions/s",
+            "frac": None if ach is None else round(ach / VALU_PEAK_GINST, 4),
+            "traffic": None if pmc is None or dom_kernel not in pmc else round(pmc[dom_kernel] * units / launches),
+            "definition": (f"{dom_kernel}: SQ_INSTS_VALU per launch ({os.path.relpath(SQ_JSON, ROOT)}, "
+                           f"commit {None if valu is None else valu.get('commit')}) / its HIP-event launch time; "
+                           f"peak = 1024 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU instruction; traffic = its "
+                           "rocprofv3 FETCH_SIZE + WRITE_SIZE bytes per launch (beyond L2, Infinity-Cache hits "
+                           "included: W is re-read per scenario pair, not an HBM fraction)"),
+            "valu_instructions_per_launch": None if valu is None else valu["SQ_INSTS_VALU"],
+            "step_bytes_beyond_l2": traffic,
+            "step_GBps_beyond_l2": None if traffic is None else round(traffic / step_s / 1e9, 1),
             "equivalent_GBps": round(equivalent, 1),
             "equivalent_definition": (f"scenario-epochs/s per GPU x the per-scenario epoch-step contract "
                                       f"{contract:,.0f} B: a rate, not traffic (every scenario reads one shared "

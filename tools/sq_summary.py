@@ -19,7 +19,9 @@ from collections import defaultdict
 ap = argparse.ArgumentParser()
 ap.add_argument("dir")
 ap.add_argument("--skip", type=int, default=0, help="first dispatches of each kernel to drop")
-ap.add_argument("--json", default=None)
+ap.add_argument("--json", default=None, help="append a record to this sq_valu.json (bench.py load_sq)")
+ap.add_argument("--workload", default=None, help='JSON of the bench workload key, e.g. {"V": 256, ...}')
+ap.add_argument("--commit", default=None)
 a = ap.parse_args()
 files = glob.glob(os.path.join(a.dir, "**", "*counter_collection*.csv"), recursive=True)
 if not files:
@@ -61,4 +63,10 @@ for k, lst in per.items():
 for k, rec in sorted(out.items(), key=lambda kv: -kv[1].get("kernel_s", 0)):
     print(k, json.dumps(rec))
 if a.json:
-    json.dump(out, open(a.json, "w"), indent=1)
+    recs = []
+    if os.path.exists(a.json):
+        recs = json.load(open(a.json))
+    wl = json.loads(a.workload) if a.workload else {}
+    recs = [r for r in recs if r.get("workload") != wl]
+    recs.append({"workload": wl, "commit": a.commit, "source": a.dir, "kernels": out})
+    json.dump(recs, open(a.json, "w"), indent=1)
