@@ -40,3 +40,27 @@ PATCHES["grp_r2_noliqsplit"] = [(
 PATCHES["cr_w3"] = [("__global__ __launch_bounds__(256, 2) void k_cons_rank", "__global__ __launch_bounds__(256, 3) void k_cons_rank")]
 # the multi-pass path (k_consensus_w + k_quantise + k_rank_s) with this source's orders
 PATCHES["cr_off"] = [("    cr_grid = cons_rank_grid(rust, tiles);", "    cr_grid = 0;")]
+# the scenario groups of one W slab (row block x tile) in consecutive blocks
+# (spread over the 8 XCDs: each XCD's L2 serves its share of the 256 groups)
+PATCHES["grp_pairminor"] = [
+    ("  const int tile = blockIdx.x % A.tiles;\n  const int rb = (blockIdx.x / A.tiles) % A.rowblocks;\n"
+     "  const int n0 = (blockIdx.x / (A.tiles * A.rowblocks)) * K;\n  const int N = A.N, V = A.V, M = A.M;\n"
+     "  const long long VM = (long long)V * M;\n  const int m = tile * kTileM + L.c4 * 4;\n  const int row0 = rb * G * R + L.g;",
+     "  const int npairs = (A.N + K - 1) / K;\n  const int tile = (blockIdx.x / npairs) % A.tiles;\n"
+     "  const int rb = (blockIdx.x / npairs) / A.tiles;\n  const int n0 = (blockIdx.x % npairs) * K;\n"
+     "  const int N = A.N, V = A.V, M = A.M;\n  const long long VM = (long long)V * M;\n"
+     "  const int m = tile * kTileM + L.c4 * 4;\n  const int row0 = rb * G * R + L.g;"),
+    ("__global__ __launch_bounds__(256, kGrpWaves) void k_bonds_grp(BondArgs A) {\n"
+     "  const int n0 = (blockIdx.x / (A.tiles * A.rowblocks)) * K;",
+     "__global__ __launch_bounds__(256, kGrpWaves) void k_bonds_grp(BondArgs A) {\n"
+     "  const int n0 = (blockIdx.x % ((A.N + K - 1) / K)) * K;")]
+PATCHES["grp_k4"] = [("constexpr int kScanGroup = 2;", "constexpr int kScanGroup = 4;")]
+PATCHES["grp_k4_w3"] = PATCHES["grp_k4"] + [("constexpr int kGrpWaves = 4;", "constexpr int kGrpWaves = 3;")]
+# c4 / c2 history-less scan: epochs in flight of the one-row scan
+PATCHES["elem_p6"] = [("    return launch_elem_shape<VARIANT, 1, VEC, 4, VEC, false, 256, 64, yk::DP_TV>(st, A);",
+                       "    return launch_elem_shape<VARIANT, 1, VEC, 6, VEC, false, 256, 64, yk::DP_TV>(st, A);")]
+PATCHES["elem_p8"] = [("    return launch_elem_shape<VARIANT, 1, VEC, 4, VEC, false, 256, 64, yk::DP_TV>(st, A);",
+                       "    return launch_elem_shape<VARIANT, 1, VEC, 8, VEC, false, 256, 64, yk::DP_TV>(st, A);")]
+PATCHES["grp_k4_r1"] = PATCHES["grp_k4"] + [("constexpr int K = kScanGroup, R = 2;", "constexpr int K = kScanGroup, R = 1;")]
+PATCHES["grp_k4_w2"] = PATCHES["grp_k4"] + [("constexpr int kGrpWaves = 4;", "constexpr int kGrpWaves = 2;")]
+PATCHES["grp_k4_r1_w3"] = PATCHES["grp_k4_r1"] + [("constexpr int kGrpWaves = 4;", "constexpr int kGrpWaves = 3;")]

@@ -2270,7 +2270,12 @@ __global__ __launch_bounds__(512, 1) void k_bonds_cn(BondArgs A) {
   __shared__ __attribute__((aligned(16))) float red[2][8][kCnStrip];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int cq = lane >> 4, rr = lane & 15;
-  const int strip = blockIdx.x % A.cblocks;
+  // Strips 2k and 2k + 1 read the two halves of every 128-byte line of their
+  // rows, and blocks b, b + 8 run on one XCD (round-robin dispatch): pair
+  // them there, or each XCD's L2 fetches the whole line for its half (PMC:
+  // 8.5 GB read per c2 launch for 4.2 GB of W)
+  int strip = blockIdx.x % A.cblocks;
+  if (strip < (A.cblocks & ~15)) strip = (strip & ~15) | ((strip & 7) << 1) | ((strip >> 3) & 1);
   const int n = blockIdx.x / A.cblocks;
   const int N = A.N, V = A.V, M = A.M;
   const long long VM = (long long)V * M;
