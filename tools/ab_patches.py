@@ -64,3 +64,58 @@ PATCHES["elem_p8"] = [("    return launch_elem_shape<VARIANT, 1, VEC, 4, VEC, fa
 PATCHES["grp_k4_r1"] = PATCHES["grp_k4"] + [("constexpr int K = kScanGroup, R = 2;", "constexpr int K = kScanGroup, R = 1;")]
 PATCHES["grp_k4_w2"] = PATCHES["grp_k4"] + [("constexpr int kGrpWaves = 4;", "constexpr int kGrpWaves = 2;")]
 PATCHES["grp_k4_r1_w3"] = PATCHES["grp_k4_r1"] + [("constexpr int kGrpWaves = 4;", "constexpr int kGrpWaves = 3;")]
+# non-temporal W loads in the element-wise scans: history-less only / every form
+PATCHES["elem_ntl"] = [("      load4c<VEC>(A.W + (A.wsh ? (long long)t : slice) * VM, rr, V, m, M, rw[k][i]);",
+                        "      load4c<VEC, !NT>(A.W + (A.wsh ? (long long)t : slice) * VM, rr, V, m, M, rw[k][i]);")]
+PATCHES["elem_ntl_all"] = [("      load4c<VEC>(A.W + (A.wsh ? (long long)t : slice) * VM, rr, V, m, M, rw[k][i]);",
+                            "      load4c<VEC, true>(A.W + (A.wsh ? (long long)t : slice) * VM, rr, V, m, M, rw[k][i]);")]
+# timing only (wrong dividends): the history-less scan without its partial stores
+PATCHES["elem_ntl_nodp"] = PATCHES["elem_ntl"] + [
+    ("          A.dpart[dp_index(DPL, slice, tile, row, A.tiles, V)] = d;",
+     "          if (d == 1234.5f) A.dpart[dp_index(DPL, slice, tile, row, A.tiles, V)] = d;")]
+# non-temporal W loads in the phase-1 readers
+_NTL_ROW = ("          const float4 t = *reinterpret_cast<const float4*>(r + m);",
+            "          const fvec4 t = __builtin_nontemporal_load(reinterpret_cast<const fvec4*>(r + m));", 2)
+_NTL_CONS = ("      const float4 t = *reinterpret_cast<const float4*>(Ws + (o0 + (unsigned)i * st));\n"
+             "      wn[i][0] = t.x;\n      wn[i][1] = t.y;\n      wn[i][2] = t.z;\n      wn[i][3] = t.w;\n    }\n  } else {\n"
+             "#pragma unroll\n    for (int i = 0; i < R; ++i) load4c<VEC>(Ws, rg + 16 * i, V, m, M, wn[i]);\n  }\n"
+             "  // the division guard's row-sum part",
+             "      const fvec4 t = __builtin_nontemporal_load(reinterpret_cast<const fvec4*>(Ws + (o0 + (unsigned)i * st)));\n"
+             "      wn[i][0] = t.x;\n      wn[i][1] = t.y;\n      wn[i][2] = t.z;\n      wn[i][3] = t.w;\n    }\n  } else {\n"
+             "#pragma unroll\n    for (int i = 0; i < R; ++i) load4c<VEC>(Ws, rg + 16 * i, V, m, M, wn[i]);\n  }\n"
+             "  // the division guard's row-sum part")
+_NTL_RANK = ("      load4c<VEC>(Ws, rr, V, m, M, w[i]);", "      load4c<VEC, true>(Ws, rr, V, m, M, w[i]);")
+PATCHES["rowsum_ntl"] = [_NTL_ROW]
+PATCHES["cons_ntl"] = [_NTL_CONS]
+PATCHES["rank_ntl"] = [_NTL_RANK]
+PATCHES["p1_ntl"] = [_NTL_ROW, _NTL_CONS, _NTL_RANK]
+PATCHES["all_ntl"] = [_NTL_ROW, _NTL_CONS, _NTL_RANK] + PATCHES["elem_ntl"]
+# timing only (wrong dividends): DP_TE scan without its gathered stores
+PATCHES["te_nostore"] = [("              A.dpart[((long long)(n * A.tiles + tile) * V + row) * A.ep + te] = gq[i];",
+                          "              if (gq[i] == 1234.5f) A.dpart[((long long)(n * A.tiles + tile) * V + row) * A.ep + te] = gq[i];")]
+# 32 epochs gathered per 16-lane row (two registers), stored as whole 128-byte lines
+PATCHES["te32"] = [
+    ("int dte_stride(int E) { return (E + 15) & ~15; }", "int dte_stride(int E) { return (E + 31) & ~31; }"),
+    ("  float gq[R];  // DP_TE: lane j of a 16-lane row holds the partial of epoch (t & ~15) + j",
+     "  float gq[R], gq2[R];  // DP_TE: lane j of a 16-lane row holds the partials of epochs (t & ~31) + j, + 16 + j"),
+    ("""          const int j = lane & 15;
+          if (j == (t & 15)) gq[i] = d;
+          if ((t & 15) == 15 || t == A.t1 - 1) {
+            const int te = (t & ~15) + j;
+            if (te >= A.t0 && te <= t && row < V && tile < A.tiles)
+              A.dpart[((long long)(n * A.tiles + tile) * V + row) * A.ep + te] = gq[i];
+          }""",
+     """          const int j = lane & 15;
+          if (j == (t & 15)) {
+            if (t & 16) gq2[i] = d;
+            else gq[i] = d;
+          }
+          if ((t & 31) == 31 || t == A.t1 - 1) {
+            const int te = (t & ~31) + j;
+            float* dq = A.dpart + ((long long)(n * A.tiles + tile) * V + row) * A.ep;
+            if (row < V && tile < A.tiles) {
+              if (te >= A.t0 && te <= t) dq[te] = gq[i];
+              if (te + 16 >= A.t0 && te + 16 <= t) dq[te + 16] = gq2[i];
+            }
+          }"""),
+]

@@ -6,14 +6,15 @@
 // access pattern's own ceiling: block size BS, tile width CB columns (CB/4
 // lanes per row), R rows per thread, P epochs of loads in flight, block order
 // (0 column-block minor, 1 row-block minor), loads plain / non-temporal,
-// partials none / [t][tile][V] (the engine's DP_TV).
+// partials none (dp0) / [t][tile][V] (dp1, the engine's DP_TV) / [tile][V][t]
+// with 16 epochs gathered per 16-lane row before one 64-B store (dp7).
 //   hipcc --offload-arch=gfx950 -O3 -o tools/scanrd tools/scanrd.hip && tools/scanrd
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 
 typedef float fvec4 __attribute__((ext_vector_type(4)));
 
-template <int BS, int CB, int R, int P, bool NTL, int ORDER, bool DP>
+template <int BS, int CB, int R, int P, bool NTL, int ORDER, int DP>
 __global__ __launch_bounds__(BS) void k_scanrd(const fvec4* __restrict__ x, int steps, int V, int M,
                                                float* out) {
   constexpr int LPR = CB / 4, G = BS / LPR;
@@ -27,12 +28,14 @@ __global__ __launch_bounds__(BS) void k_scanrd(const fvec4* __restrict__ x, int 
   for (int i = 0; i < R; ++i) off[i] = (long long)(rb * G * R + g + G * i) * m4 + tile * LPR + c;
   auto ld = [&](long long o) { return NTL ? __builtin_nontemporal_load(x + o) : x[o]; };
   fvec4 ring[P][R], acc[R];
+  float gath[R];
 #pragma unroll
   for (int i = 0; i < R; ++i) acc[i] = fvec4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int k = 0; k < P; ++k)
 #pragma unroll
     for (int i = 0; i < R; ++i) ring[k][i] = ld(k * sl + off[i]);
+  const int ep = (steps + 31) & ~31;
   for (int t0 = 0; t0 < steps; t0 += P) {
 #pragma unroll
     for (int k = 0; k < P; ++k) {
@@ -45,7 +48,16 @@ __global__ __launch_bounds__(BS) void k_scanrd(const fvec4* __restrict__ x, int 
           float p = acc[i].x + acc[i].y + acc[i].z + acc[i].w;
           for (int o = 1; o < 16; o <<= 1) p += __shfl_xor(p, o, 64);
           const int row = rb * G * R + g + G * i, st = (tile * CB + c * 4) / 64, tl = M / 64;
-          if ((threadIdx.x & 15) == 0) out[1 + ((long long)t * tl + st) * V + row] = p;
+          if (DP == 1) {
+            if ((threadIdx.x & 15) == 0) out[1 + ((long long)t * tl + st) * V + row] = p;
+          } else if (DP == 7) {
+            const int j = threadIdx.x & 15;
+            if (j == (t & 15)) gath[i] = p;
+            if ((t & 15) == 15 || t == steps - 1) {
+              const int te = (t & ~15) + j;
+              if (te <= t) out[32 + ((long long)st * V + row) * ep + te] = gath[i];
+            }
+          }
         }
         if (t + P < steps) ring[k][i] = ld((t + P) * sl + off[i]);
       }
@@ -59,11 +71,12 @@ __global__ __launch_bounds__(BS) void k_scanrd(const fvec4* __restrict__ x, int 
 
 // the rowsum-like walk for comparison: one block per (epoch, row), the row
 // read contiguously (no recurrence across epochs)
+template <bool NTL>
 __global__ __launch_bounds__(256) void k_rows(const fvec4* __restrict__ x, int M, float* out) {
   const long long base = (long long)blockIdx.x * (M / 4);
   float s = 0.f;
   for (int j = threadIdx.x; j < M / 4; j += 256) {
-    const fvec4 v = x[base + j];
+    const fvec4 v = NTL ? __builtin_nontemporal_load(x + base + j) : x[base + j];
     s += v.x + v.y + v.z + v.w;
   }
   if (s == 1234.5f) out[0] = s;
@@ -92,7 +105,7 @@ int main() {
   const long long bytes = (long long)steps * V * M * 4;  // 100 slices of 64 MiB
   fvec4* x;
   float* out;
-  if (hipMalloc(&x, bytes) != hipSuccess || hipMalloc(&out, 4 + 4ll * steps * (M / 64) * V) != hipSuccess) {
+  if (hipMalloc(&x, bytes) != hipSuccess || hipMalloc(&out, 128 + 4ll * ((steps + 31) & ~31) * (M / 64) * V) != hipSuccess) {
     fprintf(stderr, "alloc failed\n");
     return 1;
   }
@@ -112,29 +125,29 @@ int main() {
     fflush(stdout);                                                                                             \
   }
   for (int rep2 = 0; rep2 < 2; ++rep2) {
-    {
+    for (int ntl = 0; ntl < 2; ++ntl) {
       const float ms = time_ms(reps, [&] {
-        hipLaunchKernelGGL(k_rows, dim3(steps * V), dim3(256), 0, 0, x, M, out);
+        if (ntl) hipLaunchKernelGGL(k_rows<true>, dim3(steps * V), dim3(256), 0, 0, x, M, out);
+        else hipLaunchKernelGGL(k_rows<false>, dim3(steps * V), dim3(256), 0, 0, x, M, out);
       });
-      printf("rows   one block per (epoch, row)                          %7.3f ms  %6.0f GB/s\n", ms,
+      printf("rows   one block per (epoch, row) %-3s                      %7.3f ms  %6.0f GB/s\n", ntl ? "ntl" : "", ms,
              moved / ms / 1e6);
     }
-    RUN(256, 64, 1, 4, false, 0, true)  // the engine's c4 shape
-    RUN(256, 64, 1, 4, false, 0, false)
-    RUN(256, 64, 1, 4, true, 0, false)
-    RUN(256, 64, 1, 4, false, 1, false)
-    RUN(256, 64, 1, 8, false, 0, false)
-    RUN(256, 64, 2, 4, false, 0, false)
-    RUN(256, 256, 1, 4, false, 0, false)
-    RUN(256, 256, 1, 8, false, 0, false)
-    RUN(256, 1024, 1, 4, false, 0, false)
-    RUN(256, 1024, 1, 8, false, 0, false)
-    RUN(512, 1024, 1, 8, false, 0, false)
-    RUN(1024, 1024, 1, 8, false, 0, false)
-    RUN(256, 1024, 2, 4, false, 0, false)
-    RUN(256, 1024, 4, 2, false, 0, false)
-    RUN(1024, 4096, 1, 8, false, 0, false)
-    RUN(256, 256, 4, 4, false, 0, false)
+    RUN(256, 64, 1, 4, false, 0, 1)  // the engine's c4 shape
+    RUN(256, 64, 1, 4, true, 0, 1)
+    RUN(256, 64, 1, 4, true, 0, 0)
+    RUN(256, 64, 1, 4, true, 0, 7)
+    RUN(256, 64, 1, 4, false, 0, 7)
+    RUN(512, 64, 1, 4, true, 0, 1)
+    RUN(1024, 64, 1, 4, true, 0, 1)
+    RUN(256, 64, 2, 4, true, 0, 1)
+    RUN(256, 64, 2, 2, true, 0, 1)
+    RUN(256, 64, 4, 2, true, 0, 1)
+    RUN(512, 64, 1, 4, true, 0, 7)
+    RUN(256, 64, 2, 4, true, 0, 7)
+    RUN(256, 64, 1, 2, true, 0, 7)
+    RUN(256, 64, 1, 6, true, 0, 7)
+    RUN(256, 256, 1, 4, true, 0, 0)
   }
   return 0;
 }

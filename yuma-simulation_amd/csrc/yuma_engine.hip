@@ -40,6 +40,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <vector>
 
 #include "yuma_hip.h"
@@ -293,22 +294,25 @@ __device__ __forceinline__ void load4(const float* __restrict__ row, int m, int 
 }
 // Branch-free loads: out-of-range rows / columns read a clamped in-range
 // address and are zeroed afterwards, so a thread's loads issue back to back
-// instead of one HBM round trip per (divergent) row.
-template <bool VEC>
+// instead of one HBM round trip per (divergent) row. NTL: non-temporal loads
+// (streaming reads of data no later access in the launch re-reads).
+template <bool VEC, bool NTL = false>
 __device__ __forceinline__ void load4c(const float* __restrict__ base, int row, int V, int m,
                                        int M, float (&x)[4]) {
   const int rr = row < V ? row : V - 1;
   const float* r = base + (long long)rr * M;
   if (VEC) {
     const int mm = m < M ? m : M - 4;
-    const float4 t = *reinterpret_cast<const float4*>(r + mm);
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    const f4 t = NTL ? __builtin_nontemporal_load(reinterpret_cast<const f4*>(r + mm))
+                     : *reinterpret_cast<const f4*>(r + mm);
     x[0] = t.x;
     x[1] = t.y;
     x[2] = t.z;
     x[3] = t.w;
   } else {
 #pragma unroll
-    for (int c = 0; c < 4; ++c) x[c] = r[min(m + c, M - 1)];
+    for (int c = 0; c < 4; ++c) x[c] = NTL ? __builtin_nontemporal_load(r + min(m + c, M - 1)) : r[min(m + c, M - 1)];
   }
 }
 __device__ __forceinline__ void mask4(int row, int V, int m, int M, float (&x)[4]) {
@@ -350,7 +354,10 @@ __device__ __forceinline__ void load4_vec(const float* __restrict__ v, int m, in
 // the row is cut into 256-miner chunks; a chunk's partial is the balanced
 // binary tree over its 64 column quads of the sequential quad sums
 // ((x0+x1)+x2)+x3 (lane l holds quad l: the 64-lane butterfly); the chunk
-// partials are added in chunk order.
+// partials are added in chunk order. W is read with non-temporal loads: no
+// later access in the launch re-reads it (c2 0.687 -> 0.636 ms, c4 1.09 ->
+// 0.96, same box; the same loads in the consensus kernel lose, 0.87 -> 1.02:
+// there the two halves of a 128-byte line go to neighbouring waves).
 // ---------------------------------------------------------------------------
 // WIDE (rows of >= kWideChunks chunks, e.g. a 65536-miner subnet): block =
 // ONE row, its chunks dealt to the 4 waves, the chunk partials parked in LDS
@@ -408,7 +415,7 @@ __global__ __launch_bounds__(256) void k_rowsum(const float* __restrict__ W,
       float x[4];
       if (VEC) {
         if (m < M) {
-          const float4 t = *reinterpret_cast<const float4*>(r + m);
+          const fvec4 t = __builtin_nontemporal_load(reinterpret_cast<const fvec4*>(r + m));
           x[0] = t.x;
           x[1] = t.y;
           x[2] = t.z;
@@ -460,7 +467,7 @@ __global__ __launch_bounds__(256) void k_rowsum(const float* __restrict__ W,
       float x[4];
       if (VEC) {
         if (m < M) {
-          const float4 t = *reinterpret_cast<const float4*>(r + m);
+          const fvec4 t = __builtin_nontemporal_load(reinterpret_cast<const fvec4*>(r + m));
           x[0] = t.x;
           x[1] = t.y;
           x[2] = t.z;
@@ -1944,14 +1951,19 @@ struct BondArgs {
   int N, V, M, tiles, rowblocks, t0, t1;
   int wsh;      // every scenario reads input slice t (yuma_run_shared)
   int cblocks;  // k_bonds_elem: column blocks of CB miners per row block
+  int ep;       // DP_TE: epoch stride of a (scenario, tile, row) series (multiple of 16)
 };
 
 // Layouts of the per-(slice, 64-miner tile, validator) dividend partials:
 // DP_TV [slice][tile][V] (k_bonds; k_bonds_elem on 64-miner tiles), DP_VT
 // [slice][V][tile] (k_bonds_elem on wide column blocks: a wave's four
-// 64-miner tiles of one row land in 16 contiguous bytes). k_finalize / k_dsum
-// add the tiles in the same order either way.
-enum DpLayout { DP_TV = 0, DP_VT = 1 };
+// 64-miner tiles of one row land in 16 contiguous bytes), DP_TE
+// [scenario][tile][V][epoch] (the one-row history-less scan: each 16-lane row
+// gathers 16 epochs of its (tile, row) partial, one per lane, and stores them
+// as one 64-byte segment; k_dte_sum adds the tiles into DP_PRE [slice][V]).
+// k_finalize / k_dsum / k_dte_sum add the tiles in the same order in every
+// layout.
+enum DpLayout { DP_TV = 0, DP_VT = 1, DP_TE = 2, DP_PRE = 3 };
 __device__ __forceinline__ long long dp_index(int layout, long long slice, int tile, int v, int tiles,
                                               int V) {
   return layout == DP_VT ? (slice * V + v) * (long long)tiles + tile : (slice * tiles + tile) * (long long)V + v;
@@ -2559,12 +2571,16 @@ __global__ __launch_bounds__(BS, 1) void k_bonds_elem(BondArgs A) {
   }
 
   float rw[P][R][4], rd[P][R], rsn[P][R], ri[P][4], rba[P][4];
+  float gq[R];  // DP_TE: lane j of a 16-lane row holds the partial of epoch (t & ~15) + j
   auto fetch = [&](int k, int t) {
     const long long slice = (long long)t * N + n;
 #pragma unroll
     for (int i = 0; i < R; ++i) {
       const int rr = min(row0 + G * i, V - 1);
-      load4c<VEC>(A.W + (A.wsh ? (long long)t : slice) * VM, rr, V, m, M, rw[k][i]);
+      // the one-row history-less scan streams each W slice exactly once
+      // (rowsum / consensus / rank read it in their own launches): non-
+      // temporal loads (c4 bonds 1.63 -> 1.50 ms, same box)
+      load4c<VEC, DPL == DP_TE>(A.W + (A.wsh ? (long long)t : slice) * VM, rr, V, m, M, rw[k][i]);
       rd[k][i] = A.rsd[slice * V + rr];
       rsn[k][i] = A.sn[slice * V + rr];
     }
@@ -2678,8 +2694,19 @@ __global__ __launch_bounds__(BS, 1) void k_bonds_elem(BondArgs A) {
             if (m + c < M) d = d + B[i][c] * ri[k][c];
         }
         d = wsum16(d);  // sum_row16's xor-butterfly tree, on DPP
-        if ((lane & 15) == 0 && row < V && tile < A.tiles)
+        if constexpr (DPL == DP_TE) {
+          // (the [slice][tile][V] 4-byte stores cost this scan 0.24 ms at c4:
+          // timing-only build without them, 1.50 -> 1.26 ms)
+          const int j = lane & 15;
+          if (j == (t & 15)) gq[i] = d;
+          if ((t & 15) == 15 || t == A.t1 - 1) {
+            const int te = (t & ~15) + j;
+            if (te >= A.t0 && te <= t && row < V && tile < A.tiles)
+              A.dpart[((long long)(n * A.tiles + tile) * V + row) * A.ep + te] = gq[i];
+          }
+        } else if ((lane & 15) == 0 && row < V && tile < A.tiles) {
           A.dpart[dp_index(DPL, slice, tile, row, A.tiles, V)] = d;
+        }
       }
       has_old = true;
       if (t + P < A.t1) fetch(k, t + P);
@@ -3010,6 +3037,14 @@ __global__ __launch_bounds__(256) void k_finalize(const float* __restrict__ dpar
   const long long slice = slice0 + blockIdx.x;
   const int tg = threadIdx.x >> 6, vq = threadIdx.x & 63;
   const float* dp = dpart + slice * (long long)tiles * V;
+  if (dpl == DP_PRE) {  // tile sums already formed (k_dte_sum, same order)
+    for (int v = threadIdx.x; v < V; v += 256) {
+      float d = dpart[slice * V + v];
+      if (variant == YUMA_VARIANT_YUMA4) d = sn[slice * V + v] * d;
+      dsh[v] = d;
+    }
+    __syncthreads();
+  }
   if (dpl == DP_VT) {
     // [V][tile]: one thread per validator walks its contiguous tiles, keeping
     // the four tile-group sums of the [tile][V] path apart (tile k goes to
@@ -3093,6 +3128,46 @@ __global__ __launch_bounds__(256) void k_finalize(const float* __restrict__ dpar
       }
       Tv[slice * V + v] = a / b;
     }
+  }
+}
+
+// DP_TE partials -> DP_PRE tile sums for the epochs [t0, t1): out[slice][v].
+// SEQ = false: k_finalize's order (tile group g = k % 4 summed sequentially,
+// then groups 0..3: one wave per group, joined through LDS); SEQ = true:
+// k_dsum's order (tiles sequentially). Block: 16 epochs x 4 validators per
+// wave (a wave load = four 64-byte epoch runs), grid (scenario, 16-epoch
+// group, validator quad) [x4 validator quads per block for SEQ].
+template <bool SEQ>
+__global__ __launch_bounds__(256) void k_dte_sum(const float* __restrict__ dpart, int N, int V, int tiles,
+                                                 int ep, int t0, int t1, float* __restrict__ out) {
+  __shared__ float part[4][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int vgroups = SEQ ? (V + 15) / 16 : (V + 3) / 4;
+  const int tgroups = (t1 - (t0 & ~15) + 15) / 16;
+  const int vg = blockIdx.x % vgroups;
+  const int tg = (blockIdx.x / vgroups) % tgroups;
+  const int n = blockIdx.x / (vgroups * tgroups);
+  const int t = (t0 & ~15) + tg * 16 + (lane & 15);
+  const int v = SEQ ? vg * 16 + wave * 4 + (lane >> 4) : vg * 4 + (lane >> 4);
+  const bool ok = t >= t0 && t < t1 && v < V;
+  const float* p = dpart + ((long long)n * tiles * V + (ok ? v : 0)) * ep + (ok ? t : 0);
+  const long long kstride = (long long)V * ep;
+  float acc = 0.0f;
+  const int k0 = SEQ ? 0 : wave, kstep = SEQ ? 1 : 4;
+#pragma unroll 8
+  for (int k = k0; k < tiles; k += kstep) acc = acc + p[k * kstride];
+  if (SEQ) {
+    if (ok) out[((long long)t * N + n) * V + v] = acc;
+    return;
+  }
+  part[wave][lane] = acc;
+  __syncthreads();
+  if (wave == 0 && ok) {
+    float d = part[0][lane];
+    d = d + part[1][lane];
+    d = d + part[2][lane];
+    d = d + part[3][lane];
+    out[((long long)t * N + n) * V + v] = d;
   }
 }
 
@@ -3220,6 +3295,7 @@ struct Workspace {
   float* ba;
   float* rpart;
   float* dpart;
+  float* dsum;  // DP_PRE tile sums of DP_TE partials [slice][V]
   float* scal;
   float* tvc;
   float* tvn;
@@ -3236,6 +3312,8 @@ size_t partial_tiles(int variant, int M) {
   return variant <= YUMA_VARIANT_YUMA2 ? (size_t)(M + yk::kCnStrip - 1) / yk::kCnStrip
                                        : (size_t)(M + yk::kTileM - 1) / yk::kTileM;
 }
+
+int dte_stride(int E) { return (E + 15) & ~15; }
 
 Workspace carve(char* base, int variant, int N, int E, int V, int M, int full) {
   Workspace w{};
@@ -3258,7 +3336,10 @@ Workspace carve(char* base, int variant, int N, int E, int V, int M, int full) {
   w.I = (float*)take(S * M * 4);
   w.ba = (float*)take(S * M * 4);
   w.rpart = (float*)take(S * tiles * 4);
-  w.dpart = (float*)take(S * partial_tiles(variant, M) * V * 4);
+  // DP_TE pads each (scenario, tile, row) epoch series to a multiple of 16
+  const size_t dp_te = (size_t)N * tiles * V * (size_t)dte_stride(E);
+  w.dpart = (float*)take(std::max(S * partial_tiles(variant, M) * V, dp_te) * 4);
+  w.dsum = (float*)take(S * V * 4);
   w.scal = (float*)take(S * 8 * 4);
   w.tvc = full ? (float*)take(S * tiles * V * 4) : nullptr;
   w.tvn = full ? (float*)take(S * tiles * V * 4) : nullptr;
@@ -3482,7 +3563,7 @@ int launch_bonds_elem(hipStream_t st, yk::BondArgs& A) {
     }
   }
   if (bonds_rows(VEC, hist, A.wsh != 0) != 2)
-    return launch_elem_shape<VARIANT, 1, VEC, 4, VEC, false, 256, 64, yk::DP_TV>(st, A);
+    return launch_elem_shape<VARIANT, 1, VEC, 4, VEC, false, 256, 64, yk::DP_TE>(st, A);
   if (hist) return launch_elem_shape<VARIANT, 2, VEC, 2, VEC, true, 256, 64, yk::DP_TV>(st, A);
   return launch_elem_shape<VARIANT, 2, VEC, 2, VEC, false, 256, 64, yk::DP_TV>(st, A);
 }
@@ -3660,12 +3741,20 @@ int run_impl(int variant, const yuma_params_t* prm, int N, int E, int V, int M, 
     A.t0 = c0;
     A.t1 = c1;
     A.wsh = wsh;
+    A.ep = dte_stride(E);
     tm.mark(YUMA_PHASE_BONDS);
     int ptiles = tiles;
-    const int dpl = vec ? launch_bonds<true>(variant, rc, st, A, &ptiles)
-                        : launch_bonds<false>(variant, rc, st, A, &ptiles);
+    int dpl = vec ? launch_bonds<true>(variant, rc, st, A, &ptiles)
+                  : launch_bonds<false>(variant, rc, st, A, &ptiles);
     tm.mark(YUMA_PHASE_FINALIZE);
-    YK_LAUNCH(yk::k_finalize, ns, 256, st, ws.dpart, ws.sn, variant, V, s0, ptiles, ws.tvc,
+    const float* dsrc = ws.dpart;
+    if (dpl == yk::DP_TE) {
+      YK_LAUNCH(yk::k_dte_sum<false>, (long long)N * ((c1 - (c0 & ~15) + 15) / 16) * ((V + 3) / 4), 256, st,
+                ws.dpart, N, V, ptiles, A.ep, c0, c1, ws.dsum);
+      dsrc = ws.dsum;
+      dpl = yk::DP_PRE;
+    }
+    YK_LAUNCH(yk::k_finalize, ns, 256, st, dsrc, ws.sn, variant, V, s0, ptiles, ws.tvc,
               ws.tvn, out->Dn, out->D, out->Tv, dpl, tiles);
     if (out->Sn != nullptr)
       (void)hipMemcpyAsync(out->Sn + s0 * V, ws.sn + s0 * V, (size_t)ns * V * 4,
@@ -3816,10 +3905,15 @@ int shard_stage_impl(int stage, int variant, const yuma_params_t* prm, int N, in
       A.tiles = tiles;
       A.t0 = 0;
       A.t1 = E;
+      A.ep = dte_stride(E);
       int ptiles = tiles;
       const int dpl = vec ? launch_bonds<true>(variant, rc, st, A, &ptiles)
                           : launch_bonds<false>(variant, rc, st, A, &ptiles);
-      YK_LAUNCH(yk::k_dsum, ns, 256, st, ws.dpart, V, ptiles, io->dsum_part, dpl);
+      if (dpl == yk::DP_TE)
+        YK_LAUNCH(yk::k_dte_sum<true>, (long long)N * ((E + 15) / 16) * ((V + 15) / 16), 256, st, ws.dpart, N,
+                  V, ptiles, A.ep, 0, E, io->dsum_part);
+      else
+        YK_LAUNCH(yk::k_dsum, ns, 256, st, ws.dpart, V, ptiles, io->dsum_part, dpl);
       break;
     }
     case 5: {
