@@ -66,7 +66,15 @@ def phase_bytes(phase: str, V: int, M: int, variant: int, liquid: bool, hist: bo
     and the per-epoch row sums are read once per input epoch for all of them,
     so their bytes are divided among the wshare scenarios."""
     tiles = (M + 63) // 64
-    ptiles = (M + 15) // 16 if variant <= 2 else tiles  # dividend partials per (slice, validator)
+    # dividend partials per (slice, validator): 16-miner strips (column-
+    # normalised strip scan), quads of 64-miner tiles (the wide history scan
+    # and the history-less one-row scan), else one per tile (the sweep scan)
+    if variant <= 2:
+        ptiles = (M + 15) // 16
+    elif wshare == 1 and (not hist or M >= 1024):
+        ptiles = (tiles + 3) // 4
+    else:
+        ptiles = tiles
     VM = V * M
     colnorm = variant <= 2
     w = 4 * VM / wshare

@@ -119,3 +119,29 @@ PATCHES["te32"] = [
             }
           }"""),
 ]
+# k_bonds_elem: settle every pre-loop load (bond state, ring prefetch) before the
+# epoch loop, so the waitcnt pass need not drain the ring in the loop
+_ELEM_PRE = """#pragma unroll
+  for (int k = 0; k < P; ++k)
+    if (A.t0 + k < A.t1) fetch(k, A.t0 + k);
+
+  for (int tb = A.t0; tb < A.t1; tb += P) {"""
+PATCHES["elem_wait0"] = [(_ELEM_PRE, _ELEM_PRE.replace("\n\n  for (int tb", "\n  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)\n\n  for (int tb"))]
+# ... and every ring refill unconditional (clamped to the last epoch), the
+# liquid bond_alpha load unconditional (a valid dummy address when fixed)
+PATCHES["elem_uncond"] = PATCHES["elem_wait0"] + [
+    ("      if (liquid) load4c<true>(A.ba + slice * M, 0, 1, m, M, rba[k]);",
+     "      load4c<true>((liquid ? A.ba : A.I) + slice * M, 0, 1, m, M, rba[k]);"),
+    ("      has_old = true;\n      if (t + P < A.t1) fetch(k, t + P);",
+     "      has_old = true;\n      fetch(k, min(t + P, A.t1 - 1));"),
+]
+# waitcnt diagnostics (compile-only; wrong results)
+_NOHIST = ("        if (A.B_hist != nullptr && row < V) {\n          float* hp = A.B_hist + slice * VM + (long long)row * M;",
+           "        if (false) {\n          float* hp = A.B_hist + slice * VM + (long long)row * M;")
+_NOTE = ("              A.dpart[((long long)(n * A.tiles + tile) * V + row) * A.ep + te] = gq[i];",
+         "              (void)0;")
+_NORESET = ("          fire = A.C[(slice - N) * M + reset_index] == 0.0f;\n        const int c = reset_index - m;", "          fire = false;\n        const int c = reset_index - m;")
+PATCHES["wc_a"] = PATCHES["elem_uncond"] + [_NOHIST]
+PATCHES["wc_b"] = PATCHES["elem_uncond"] + [_NOTE]
+PATCHES["wc_c"] = PATCHES["elem_uncond"] + [_NORESET]
+PATCHES["wc_d"] = PATCHES["elem_uncond"] + [_NOHIST, _NOTE, _NORESET]

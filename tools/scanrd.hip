@@ -7,14 +7,19 @@
 // lanes per row), R rows per thread, P epochs of loads in flight, block order
 // (0 column-block minor, 1 row-block minor), loads plain / non-temporal,
 // partials none (dp0) / [t][tile][V] (dp1, the engine's DP_TV) / [tile][V][t]
-// with 16 epochs gathered per 16-lane row before one 64-B store (dp7).
+// with 16 epochs gathered per 16-lane row before one 64-B store (dp7), 32
+// epochs per two stores (dp8), the partials reduced but never stored (dp10),
+// stored to an L2-resident 1 MiB buffer overwritten every epoch (dp11);
+// RED 0 shuffle butterfly, 1 DPP row butterfly. dp12 / dp13: four 64-miner
+// tiles summed per wave (CB = 256: one row per wave) and stored per epoch
+// [t][quad][V] / gathered over 16 epochs [quad][V][t].
 //   hipcc --offload-arch=gfx950 -O3 -o tools/scanrd tools/scanrd.hip && tools/scanrd
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 
 typedef float fvec4 __attribute__((ext_vector_type(4)));
 
-template <int BS, int CB, int R, int P, bool NTL, int ORDER, int DP>
+template <int BS, int CB, int R, int P, bool NTL, int ORDER, int DP, int RED = 0>
 __global__ __launch_bounds__(BS) void k_scanrd(const fvec4* __restrict__ x, int steps, int V, int M,
                                                float* out) {
   constexpr int LPR = CB / 4, G = BS / LPR;
@@ -28,7 +33,7 @@ __global__ __launch_bounds__(BS) void k_scanrd(const fvec4* __restrict__ x, int 
   for (int i = 0; i < R; ++i) off[i] = (long long)(rb * G * R + g + G * i) * m4 + tile * LPR + c;
   auto ld = [&](long long o) { return NTL ? __builtin_nontemporal_load(x + o) : x[o]; };
   fvec4 ring[P][R], acc[R];
-  float gath[R];
+  float gath[R], gath2[R];
 #pragma unroll
   for (int i = 0; i < R; ++i) acc[i] = fvec4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -46,7 +51,14 @@ __global__ __launch_bounds__(BS) void k_scanrd(const fvec4* __restrict__ x, int 
         acc[i] = acc[i] * 0.5f + ring[k][i];
         if (DP) {
           float p = acc[i].x + acc[i].y + acc[i].z + acc[i].w;
-          for (int o = 1; o < 16; o <<= 1) p += __shfl_xor(p, o, 64);
+          if (RED == 0) {
+            for (int o = 1; o < 16; o <<= 1) p += __shfl_xor(p, o, 64);
+          } else {
+            p += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, p), 0xB1, 0xF, 0xF, false));
+            p += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, p), 0x4E, 0xF, 0xF, false));
+            p += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, p), 0x141, 0xF, 0xF, false));
+            p += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, p), 0x140, 0xF, 0xF, false));
+          }
           const int row = rb * G * R + g + G * i, st = (tile * CB + c * 4) / 64, tl = M / 64;
           if (DP == 1) {
             if ((threadIdx.x & 15) == 0) out[1 + ((long long)t * tl + st) * V + row] = p;
@@ -57,6 +69,36 @@ __global__ __launch_bounds__(BS) void k_scanrd(const fvec4* __restrict__ x, int 
               const int te = (t & ~15) + j;
               if (te <= t) out[32 + ((long long)st * V + row) * ep + te] = gath[i];
             }
+          } else if (DP == 8) {
+            const int j = threadIdx.x & 15;
+            if (j == (t & 15)) {
+              if (t & 16) gath2[i] = p;
+              else gath[i] = p;
+            }
+            if ((t & 31) == 31 || t == steps - 1) {
+              const int te = (t & ~31) + j;
+              float* o = out + 32 + ((long long)st * V + row) * ep;
+              if (te <= t) o[te] = gath[i];
+              if (te + 16 <= t) o[te + 16] = gath2[i];
+            }
+          } else if (DP == 12 || DP == 13) {
+            float q = p + __shfl_xor(p, 16, 64);
+            q = q + __shfl_xor(q, 32, 64);
+            const int quad = (tile * CB) / 256, nq = M / 256;
+            if (DP == 12) {
+              if ((threadIdx.x & 63) == 0) out[1 + ((long long)t * nq + quad) * V + row] = q;
+            } else {
+              const int j = threadIdx.x & 63;
+              if (j == (t & 15)) gath[i] = q;
+              if ((t & 15) == 15 || t == steps - 1) {
+                const int te = (t & ~15) + j;
+                if (j < 16 && te <= t) out[32 + ((long long)quad * V + row) * ep + te] = gath[i];
+              }
+            }
+          } else if (DP == 10) {
+            if ((threadIdx.x & 15) == 0 && p == 1234.5f) out[1 + ((long long)t * tl + st) * V + row] = p;
+          } else if (DP == 11) {
+            if ((threadIdx.x & 15) == 0) out[1 + ((long long)(st & 1023)) * V + row] = p;
           }
         }
         if (t + P < steps) ring[k][i] = ld((t + P) * sl + off[i]);
@@ -112,16 +154,16 @@ int main() {
   (void)hipMemset(x, 0, bytes);
   const double moved = (double)bytes;
   const int reps = 5;
-#define RUN(BS, CB, R, P, NTL, ORDER, DP)                                                                         \
+#define RUN(BS, CB, R, P, NTL, ORDER, DP, RED)                                                                         \
   {                                                                                                             \
     constexpr int G = BS / (CB / 4);                                                                            \
     const int blocks = (V / (G * R)) * (M / CB);                                                                \
     const float ms = time_ms(reps, [&] {                                                                        \
-      hipLaunchKernelGGL((k_scanrd<BS, CB, R, P, NTL, ORDER, DP>), dim3(blocks), dim3(BS), 0, 0, x, steps, V, M, \
+      hipLaunchKernelGGL((k_scanrd<BS, CB, R, P, NTL, ORDER, DP, RED>), dim3(blocks), dim3(BS), 0, 0, x, steps, V, M, \
                          out);                                                                                  \
     });                                                                                                         \
-    printf("scanrd BS%-5d CB%-5d R%d P%d %-3s order%d dp%d %6d blocks (%3d rows x %5d B)  %7.3f ms  %6.0f GB/s\n", \
-           BS, CB, R, P, NTL ? "ntl" : "", ORDER, DP, blocks, G * R, CB * 4, ms, moved / ms / 1e6);              \
+    printf("scanrd BS%-5d CB%-5d R%d P%d %-3s order%d dp%-2d red%d %6d blocks (%3d rows x %5d B)  %7.3f ms  %6.0f GB/s\n", \
+           BS, CB, R, P, NTL ? "ntl" : "", ORDER, DP, RED, blocks, G * R, CB * 4, ms, moved / ms / 1e6);              \
     fflush(stdout);                                                                                             \
   }
   for (int rep2 = 0; rep2 < 2; ++rep2) {
@@ -133,21 +175,15 @@ int main() {
       printf("rows   one block per (epoch, row) %-3s                      %7.3f ms  %6.0f GB/s\n", ntl ? "ntl" : "", ms,
              moved / ms / 1e6);
     }
-    RUN(256, 64, 1, 4, false, 0, 1)  // the engine's c4 shape
-    RUN(256, 64, 1, 4, true, 0, 1)
-    RUN(256, 64, 1, 4, true, 0, 0)
-    RUN(256, 64, 1, 4, true, 0, 7)
-    RUN(256, 64, 1, 4, false, 0, 7)
-    RUN(512, 64, 1, 4, true, 0, 1)
-    RUN(1024, 64, 1, 4, true, 0, 1)
-    RUN(256, 64, 2, 4, true, 0, 1)
-    RUN(256, 64, 2, 2, true, 0, 1)
-    RUN(256, 64, 4, 2, true, 0, 1)
-    RUN(512, 64, 1, 4, true, 0, 7)
-    RUN(256, 64, 2, 4, true, 0, 7)
-    RUN(256, 64, 1, 2, true, 0, 7)
-    RUN(256, 64, 1, 6, true, 0, 7)
-    RUN(256, 256, 1, 4, true, 0, 0)
+    RUN(256, 64, 1, 4, true, 0, 0, 1)
+    RUN(256, 64, 1, 4, true, 0, 7, 1)   // the engine's DP_TE
+    RUN(256, 256, 1, 4, true, 0, 0, 1)
+    RUN(256, 256, 1, 4, true, 0, 10, 1)
+    RUN(256, 256, 1, 4, true, 0, 12, 1)
+    RUN(256, 256, 1, 4, true, 0, 13, 1)
+    RUN(256, 256, 2, 4, true, 0, 13, 1)
+    RUN(256, 256, 1, 6, true, 0, 13, 1)
+    RUN(512, 256, 1, 4, true, 0, 13, 1)
   }
   return 0;
 }

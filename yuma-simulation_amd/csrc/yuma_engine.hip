@@ -1951,22 +1951,45 @@ struct BondArgs {
   int N, V, M, tiles, rowblocks, t0, t1;
   int wsh;      // every scenario reads input slice t (yuma_run_shared)
   int cblocks;  // k_bonds_elem: column blocks of CB miners per row block
-  int ep;       // DP_TE: epoch stride of a (scenario, tile, row) series (multiple of 16)
+  int ep;       // DP_QTE: epoch stride of a (scenario, quad, row) series (multiple of 16)
 };
 
-// Layouts of the per-(slice, 64-miner tile, validator) dividend partials:
-// DP_TV [slice][tile][V] (k_bonds; k_bonds_elem on 64-miner tiles), DP_VT
-// [slice][V][tile] (k_bonds_elem on wide column blocks: a wave's four
-// 64-miner tiles of one row land in 16 contiguous bytes), DP_TE
-// [scenario][tile][V][epoch] (the one-row history-less scan: each 16-lane row
-// gathers 16 epochs of its (tile, row) partial, one per lane, and stores them
-// as one 64-byte segment; k_dte_sum adds the tiles into DP_PRE [slice][V]).
-// k_finalize / k_dsum / k_dte_sum add the tiles in the same order in every
-// layout.
-enum DpLayout { DP_TV = 0, DP_VT = 1, DP_TE = 2, DP_PRE = 3 };
-__device__ __forceinline__ long long dp_index(int layout, long long slice, int tile, int v, int tiles,
-                                              int V) {
-  return layout == DP_VT ? (slice * V + v) * (long long)tiles + tile : (slice * tiles + tile) * (long long)V + v;
+// Dividend partials. Each bond scan forms p_k = sum over tile k's columns of
+// B·I per (slice, validator) -- k a 64-miner tile, or the column-normalised
+// strip scan's 16-miner strip -- and D[v] of a slice is their canonical sum
+// (dp_quad / dp_canon): quads Q_b = (p_4b + p_4b+1) + (p_4b+2 + p_4b+3)
+// (absent tiles 0), S_g = sequential sum over the quads b = g (mod 4), then
+// D = ((S_0 + S_1) + S_2) + S_3. Every layout gives the same bits:
+//   DP_TV  [slice][tile][V]  per tile (k_bonds, k_bonds_cn, k_bonds_grp,
+//          k_bonds_elem on 64-miner tiles)
+//   DP_VQ  [slice][V][quad]  the wide history scan: a wave holds one quad of a
+//          row and stores Q_b (a quarter of the partial bytes)
+//   DP_QTE [scenario][quad][V][epoch]  the one-row history-less scan: Q_b of 16
+//          epochs gathered in one 16-lane row and stored as one 64-byte run
+//          (partial stores into HBM cost a read stream far more than their
+//          bytes: tools/scanrd, profiles/r04/scanrd*.txt)
+//   DP_PRE [slice][V]        D itself (k_dte_sum)
+enum DpLayout { DP_TV = 0, DP_VQ = 1, DP_QTE = 2, DP_PRE = 3 };
+__host__ __device__ __forceinline__ int dp_quads(int tiles) { return (tiles + 3) >> 2; }
+// Q_b of validator v from per-tile partials pv[k * stride]
+__device__ __forceinline__ float dp_quad(const float* __restrict__ pv, long long stride, int b, int tiles) {
+  float x[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) x[j] = 4 * b + j < tiles ? pv[(4 * b + j) * stride] : 0.0f;
+  return (x[0] + x[1]) + (x[2] + x[3]);
+}
+__device__ __forceinline__ long long dp_index(long long slice, int tile, int v, int tiles, int V) {
+  return (slice * tiles + tile) * (long long)V + v;
+}
+// YUMA_RESET_IF_ZERO_CONSENSUS (simulation_utils.py:62-88): is C of the epoch
+// before the reset epoch zero at the reset column? (false when the reset
+// epoch is outside this launch's epochs or the mode does not test C)
+__device__ __forceinline__ bool reset_c_zero(const BondArgs& A, int n, int mode, bool all, int epoch,
+                                             int index) {
+  if (mode != YUMA_RESET_IF_ZERO_CONSENSUS || all || epoch < 1 || epoch < A.t0 || epoch >= A.t1 ||
+      index < 0 || index >= A.M)
+    return false;
+  return A.C[((long long)(epoch - 1) * A.N + n) * A.M + index] == 0.0f;
 }
 
 template <int VARIANT, int NT, int R, bool VEC>
@@ -2553,6 +2576,11 @@ __global__ __launch_bounds__(BS, 1) void k_bonds_elem(BondArgs A) {
   const float p_bond_alpha = pg.bond_alpha, p_omba = pg.one_minus_bond_alpha;
   const float p_maxint = pg.maxint, p_capacity_alpha = pg.capacity_alpha, p_decay_keep = pg.decay_keep;
   const int row0 = rb * G * R + g;
+  // the conditional reset's test (C of the previous epoch at the reset
+  // column), read before the epoch loop: a load in the loop's rare reset
+  // branch made the waitcnt pass drain the whole prefetch ring (vmcnt(0))
+  // at every epoch, stores included
+  const bool zero_c = reset_c_zero(A, n, reset_mode, reset_all, reset_epoch, reset_index);
 
   float B[R][4];
   bool has_old;
@@ -2571,7 +2599,7 @@ __global__ __launch_bounds__(BS, 1) void k_bonds_elem(BondArgs A) {
   }
 
   float rw[P][R][4], rd[P][R], rsn[P][R], ri[P][4], rba[P][4];
-  float gq[R];  // DP_TE: lane j of a 16-lane row holds the partial of epoch (t & ~15) + j
+  float gq[R];  // DP_QTE: lane j < 16 holds the quad partial of epoch (t & ~15) + j
   auto fetch = [&](int k, int t) {
     const long long slice = (long long)t * N + n;
 #pragma unroll
@@ -2580,7 +2608,7 @@ __global__ __launch_bounds__(BS, 1) void k_bonds_elem(BondArgs A) {
       // the one-row history-less scan streams each W slice exactly once
       // (rowsum / consensus / rank read it in their own launches): non-
       // temporal loads (c4 bonds 1.63 -> 1.50 ms, same box)
-      load4c<VEC, DPL == DP_TE>(A.W + (A.wsh ? (long long)t : slice) * VM, rr, V, m, M, rw[k][i]);
+      load4c<VEC, DPL == DP_QTE>(A.W + (A.wsh ? (long long)t : slice) * VM, rr, V, m, M, rw[k][i]);
       rd[k][i] = A.rsd[slice * V + rr];
       rsn[k][i] = A.sn[slice * V + rr];
     }
@@ -2606,8 +2634,7 @@ __global__ __launch_bounds__(BS, 1) void k_bonds_elem(BondArgs A) {
       if (has_old && reset_mode != YUMA_RESET_NONE && t == reset_epoch &&
           (reset_all || (reset_index >= 0 && reset_index < M))) {
         bool fire = reset_mode == YUMA_RESET_ALWAYS;
-        if (reset_mode == YUMA_RESET_IF_ZERO_CONSENSUS && t >= 1 && !reset_all)
-          fire = A.C[(slice - N) * M + reset_index] == 0.0f;
+        if (reset_mode == YUMA_RESET_IF_ZERO_CONSENSUS && t >= 1 && !reset_all) fire = zero_c;
         const int c = reset_index - m;
         if (fire && (reset_all || (c >= 0 && c < 4)))
 #pragma unroll
@@ -2694,18 +2721,28 @@ __global__ __launch_bounds__(BS, 1) void k_bonds_elem(BondArgs A) {
             if (m + c < M) d = d + B[i][c] * ri[k][c];
         }
         d = wsum16(d);  // sum_row16's xor-butterfly tree, on DPP
-        if constexpr (DPL == DP_TE) {
-          // (the [slice][tile][V] 4-byte stores cost this scan 0.24 ms at c4:
-          // timing-only build without them, 1.50 -> 1.26 ms)
-          const int j = lane & 15;
-          if (j == (t & 15)) gq[i] = d;
-          if ((t & 15) == 15 || t == A.t1 - 1) {
-            const int te = (t & ~15) + j;
-            if (te >= A.t0 && te <= t && row < V && tile < A.tiles)
-              A.dpart[((long long)(n * A.tiles + tile) * V + row) * A.ep + te] = gq[i];
+        if constexpr (DPL == DP_QTE || DPL == DP_VQ) {
+          // the wave holds one quad of this row (CB >= 256, LPR >= 64):
+          // Q = (p0 + p1) + (p2 + p3) in every lane (xor butterflies pair
+          // back, a + b == b + a)
+          static_assert(LPR >= 64, "a quad partial needs one row per wave");
+          float q = d + __shfl_xor(d, 16, 64);
+          q = q + __shfl_xor(q, 32, 64);
+          const int quad = m >> 8, nq = dp_quads(A.tiles);
+          if constexpr (DPL == DP_QTE) {
+            // (the [slice][tile][V] 4-byte stores cost this scan 0.24 ms at
+            // c4: timing-only build without them, 1.50 -> 1.26 ms)
+            if (lane == (t & 15)) gq[i] = q;
+            if ((t & 15) == 15 || t == A.t1 - 1) {
+              const int te = (t & ~15) + lane;
+              if (lane < 16 && te >= A.t0 && te <= t && row < V && quad < nq)
+                A.dpart[((long long)(n * nq + quad) * V + row) * A.ep + te] = gq[i];
+            }
+          } else if (lane == 0 && row < V && quad < nq) {
+            A.dpart[(slice * V + row) * (long long)nq + quad] = q;
           }
         } else if ((lane & 15) == 0 && row < V && tile < A.tiles) {
-          A.dpart[dp_index(DPL, slice, tile, row, A.tiles, V)] = d;
+          A.dpart[dp_index(slice, tile, row, A.tiles, V)] = d;
         }
       }
       has_old = true;
@@ -2738,11 +2775,15 @@ __global__ __launch_bounds__(BS, 1) void k_bonds_elem(BondArgs A) {
 //    bond_alpha / 1 - bond_alpha as block-uniform operands; liquid (or mixed)
 //    blocks the per-miner operands with the exact one_minus_bond_alpha
 //    correction for their fixed-alpha scenarios (p_corr);
-// History (round 3): K = 2 beats 1 / 3 / 4 / 8 (profiles/r03/ab/
+// History: round 3 K = 2 beat 1 / 3 / 4 / 8 (profiles/r03/ab/
 // c3_scan_group_k.txt); packed-pair f32 math and an XCD-grouped block order
-// lost.
+// lost. Round 4 (rq4, R = 2, liquid split): K = 4 at 3 waves / SIMD (144 /
+// 168 VGPRs, 6 VGPRs spilled for Yuma 4) 6.90-6.97 ms against 7.03-7.22 for
+// K = 2 at 4 waves; K = 4 at 2 waves 8.96, K = 4 with R = 1 9.36; the
+// scenario groups of one W slab in consecutive blocks 7.15-7.17
+// (profiles/r04/ab_round3.txt, ab_round4.txt).
 // ---------------------------------------------------------------------------
-constexpr int kGrpWaves = 4;  // minimum waves per SIMD of the sweep scan (R = 2: 120 VGPRs)
+constexpr int kGrpWaves = 3;  // minimum waves per SIMD of the sweep scan
 template <int VARIANT, int K, int R, int P, bool LIQ>
 __device__ __forceinline__ void grp_scan(const BondArgs& A, unsigned liquid_mask) {
   constexpr int G = 16;
@@ -2774,6 +2815,12 @@ __device__ __forceinline__ void grp_scan(const BondArgs& A, unsigned liquid_mask
     p_rindex[k] = pg.reset_index;
     if (pg.flags & YUMA_FLAG_RESET_ALL_COLUMNS) rall_mask |= 1u << k;
   }
+  // the conditional resets' tests, read before the epoch loop (k_bonds_elem)
+  unsigned zc_mask = 0;
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+    if (k < nk && reset_c_zero(A, n0 + k, p_rmode[k], (rall_mask >> k) & 1u, p_repoch[k], p_rindex[k]))
+      zc_mask |= 1u << k;
 
   float B[K][R][4];
   bool has_old;
@@ -2925,10 +2972,8 @@ __device__ __forceinline__ void grp_scan(const BondArgs& A, unsigned liquid_mask
         const int reset_mode = p_rmode[k], reset_index = p_rindex[k];
         if (__builtin_expect(t == p_repoch[k] && has_old && reset_mode != YUMA_RESET_NONE &&
                                  (reset_all || (reset_index >= 0 && reset_index < M)), 0)) {
-          const long long slice = (long long)t * N + n0 + k;
           bool fire = reset_mode == YUMA_RESET_ALWAYS;
-          if (reset_mode == YUMA_RESET_IF_ZERO_CONSENSUS && t >= 1 && !reset_all)
-            fire = A.C[(slice - N) * M + reset_index] == 0.0f;
+          if (reset_mode == YUMA_RESET_IF_ZERO_CONSENSUS && t >= 1 && !reset_all) fire = (zc_mask >> k) & 1u;
           const int c = reset_index - m;
           if (fire && (reset_all || (c >= 0 && c < 4)))
 #pragma unroll
@@ -3028,16 +3073,16 @@ __global__ __launch_bounds__(256) void k_finalize(const float* __restrict__ dpar
                                                   const float* __restrict__ tvn,
                                                   float* __restrict__ Dn, float* __restrict__ D,
                                                   float* __restrict__ Tv, int dpl, int ttiles) {
-  // thread (tg, vq): tile group tg = tid / 64 sums tiles tg, tg+4, ...; vq owns
-  // validators 4vq..4vq+3 of the current 256-validator window. Fixed order:
-  // per-group sequential, then groups 0..3.
+  // thread (tg, vq): quad group tg = tid / 64 sums the quads tg, tg+4, ...;
+  // vq owns validators 4vq..4vq+3 of the current 256-validator window. The
+  // canonical order (dp_quad): per-group sequential, then groups 0..3.
   __shared__ float part[4][256];
   __shared__ float red[4];
   __shared__ float dsh[YUMA_MAX_VALIDATORS];
   const long long slice = slice0 + blockIdx.x;
   const int tg = threadIdx.x >> 6, vq = threadIdx.x & 63;
-  const float* dp = dpart + slice * (long long)tiles * V;
-  if (dpl == DP_PRE) {  // tile sums already formed (k_dte_sum, same order)
+  const int nq = dp_quads(tiles);
+  if (dpl == DP_PRE) {  // D already formed (k_dte_sum, same order)
     for (int v = threadIdx.x; v < V; v += 256) {
       float d = dpart[slice * V + v];
       if (variant == YUMA_VARIANT_YUMA4) d = sn[slice * V + v] * d;
@@ -3045,25 +3090,25 @@ __global__ __launch_bounds__(256) void k_finalize(const float* __restrict__ dpar
     }
     __syncthreads();
   }
-  if (dpl == DP_VT) {
-    // [V][tile]: one thread per validator walks its contiguous tiles, keeping
-    // the four tile-group sums of the [tile][V] path apart (tile k goes to
-    // group k % 4), then adds the groups in order: the same bits
+  if (dpl == DP_VQ) {
+    // [V][quad]: one thread per validator walks its contiguous quads, keeping
+    // the four group sums apart (quad b goes to group b % 4)
+    const float* dq = dpart + slice * (long long)nq * V;
     for (int v = threadIdx.x; v < V; v += 256) {
-      const float* pv = dp + (long long)v * tiles;
+      const float* pv = dq + (long long)v * nq;
       float pg[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-      int k = 0;
-      if ((tiles & 3) == 0) {
+      int b = 0;
+      if ((nq & 3) == 0) {
 #pragma unroll 4
-        for (; k < tiles; k += 4) {
-          const float4 x = *reinterpret_cast<const float4*>(pv + k);
+        for (; b < nq; b += 4) {
+          const float4 x = *reinterpret_cast<const float4*>(pv + b);
           pg[0] = pg[0] + x.x;
           pg[1] = pg[1] + x.y;
           pg[2] = pg[2] + x.z;
           pg[3] = pg[3] + x.w;
         }
       } else {
-        for (; k < tiles; ++k) pg[k & 3] = pg[k & 3] + pv[k];
+        for (; b < nq; ++b) pg[b & 3] = pg[b & 3] + pv[b];
       }
       float d = pg[0];
       d = d + pg[1];
@@ -3074,26 +3119,31 @@ __global__ __launch_bounds__(256) void k_finalize(const float* __restrict__ dpar
     }
     __syncthreads();
   }
+  const float* dp = dpart + slice * (long long)tiles * V;
   for (int v0 = 0; v0 < V && dpl == DP_TV; v0 += 256) {
     float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
     const int vb = v0 + vq * 4;
     if ((V & 3) == 0 && vb < V) {
-      // whole validator quads: float4 loads, 8 tiles in flight (a wide
-      // subnet has 1024 tiles per slice; same per-group sequential order)
-#pragma unroll 8
-      for (int k = tg; k < tiles; k += 4) {
-        const float4 x = *reinterpret_cast<const float4*>(dp + (long long)k * V + vb);
-        acc[0] = acc[0] + x.x;
-        acc[1] = acc[1] + x.y;
-        acc[2] = acc[2] + x.z;
-        acc[3] = acc[3] + x.w;
+      // whole validator quads: float4 loads of a quad's four tiles, two quads
+      // in flight (a wide subnet has 256 quads per slice)
+#pragma unroll 2
+      for (int b = tg; b < nq; b += 4) {
+        float4 x[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          x[j] = 4 * b + j < tiles ? *reinterpret_cast<const float4*>(dp + (long long)(4 * b + j) * V + vb)
+                                   : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        acc[0] = acc[0] + ((x[0].x + x[1].x) + (x[2].x + x[3].x));
+        acc[1] = acc[1] + ((x[0].y + x[1].y) + (x[2].y + x[3].y));
+        acc[2] = acc[2] + ((x[0].z + x[1].z) + (x[2].z + x[3].z));
+        acc[3] = acc[3] + ((x[0].w + x[1].w) + (x[2].w + x[3].w));
       }
     } else {
-      for (int k = tg; k < tiles; k += 4) {
+      for (int b = tg; b < nq; b += 4) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int v = vb + j;
-          if (v < V) acc[j] = acc[j] + dp[(long long)k * V + v];
+          if (v < V) acc[j] = acc[j] + dp_quad(dp + v, V, b, tiles);
         }
       }
     }
@@ -3131,35 +3181,29 @@ __global__ __launch_bounds__(256) void k_finalize(const float* __restrict__ dpar
   }
 }
 
-// DP_TE partials -> DP_PRE tile sums for the epochs [t0, t1): out[slice][v].
-// SEQ = false: k_finalize's order (tile group g = k % 4 summed sequentially,
-// then groups 0..3: one wave per group, joined through LDS); SEQ = true:
-// k_dsum's order (tiles sequentially). Block: 16 epochs x 4 validators per
-// wave (a wave load = four 64-byte epoch runs), grid (scenario, 16-epoch
-// group, validator quad) [x4 validator quads per block for SEQ].
-template <bool SEQ>
+// DP_QTE quad partials -> D (DP_PRE) for the epochs [t0, t1): out[slice][v]
+// in the canonical order (one wave per quad group g = b % 4, summed
+// sequentially, the groups joined in order through LDS). Block: 16 epochs x
+// 4 validators per wave (a wave load = four 64-byte epoch runs), grid
+// (scenario, 16-epoch group, validator quad).
 __global__ __launch_bounds__(256) void k_dte_sum(const float* __restrict__ dpart, int N, int V, int tiles,
                                                  int ep, int t0, int t1, float* __restrict__ out) {
   __shared__ float part[4][64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int vgroups = SEQ ? (V + 15) / 16 : (V + 3) / 4;
+  const int nq = dp_quads(tiles);
+  const int vgroups = (V + 3) / 4;
   const int tgroups = (t1 - (t0 & ~15) + 15) / 16;
   const int vg = blockIdx.x % vgroups;
   const int tg = (blockIdx.x / vgroups) % tgroups;
   const int n = blockIdx.x / (vgroups * tgroups);
   const int t = (t0 & ~15) + tg * 16 + (lane & 15);
-  const int v = SEQ ? vg * 16 + wave * 4 + (lane >> 4) : vg * 4 + (lane >> 4);
+  const int v = vg * 4 + (lane >> 4);
   const bool ok = t >= t0 && t < t1 && v < V;
-  const float* p = dpart + ((long long)n * tiles * V + (ok ? v : 0)) * ep + (ok ? t : 0);
-  const long long kstride = (long long)V * ep;
+  const float* p = dpart + ((long long)n * nq * V + (ok ? v : 0)) * ep + (ok ? t : 0);
+  const long long bstride = (long long)V * ep;
   float acc = 0.0f;
-  const int k0 = SEQ ? 0 : wave, kstep = SEQ ? 1 : 4;
 #pragma unroll 8
-  for (int k = k0; k < tiles; k += kstep) acc = acc + p[k * kstride];
-  if (SEQ) {
-    if (ok) out[((long long)t * N + n) * V + v] = acc;
-    return;
-  }
+  for (int b = wave; b < nq; b += 4) acc = acc + p[b * bstride];
   part[wave][lane] = acc;
   __syncthreads();
   if (wave == 0 && ok) {
@@ -3212,13 +3256,34 @@ __global__ __launch_bounds__(64) void k_rsum(const float* __restrict__ rpart, in
     out[slice] = s;
   }
 }
-// per slice and validator: sum over this shard's tiles of the dividend partials
+// per slice and validator: sum over this shard's tiles of [slice][tile][V]
+// partials (validator-trust numerators / denominators), sequentially
 __global__ __launch_bounds__(256) void k_dsum(const float* __restrict__ dpart, int V, int tiles,
-                                              float* __restrict__ out, int dpl) {
+                                              float* __restrict__ out) {
   const long long slice = blockIdx.x;
   for (int v = threadIdx.x; v < V; v += 256) {
     float d = 0.0f;
-    for (int k = 0; k < tiles; ++k) d = d + dpart[dp_index(dpl, slice, k, v, tiles, V)];
+    for (int k = 0; k < tiles; ++k) d = d + dpart[dp_index(slice, k, v, tiles, V)];
+    out[slice * V + v] = d;
+  }
+}
+// per slice and validator: this shard's dividend partials (DP_TV / DP_VQ) in
+// the canonical order (k_finalize)
+__global__ __launch_bounds__(256) void k_dsum_canon(const float* __restrict__ dpart, int V, int tiles,
+                                                    float* __restrict__ out, int dpl) {
+  const long long slice = blockIdx.x;
+  const int nq = dp_quads(tiles);
+  for (int v = threadIdx.x; v < V; v += 256) {
+    float pg[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    for (int b = 0; b < nq; ++b) {
+      const float q = dpl == DP_VQ ? dpart[(slice * V + v) * nq + b]
+                                   : dp_quad(dpart + slice * (long long)tiles * V + v, V, b, tiles);
+      pg[b & 3] = pg[b & 3] + q;
+    }
+    float d = pg[0];
+    d = d + pg[1];
+    d = d + pg[2];
+    d = d + pg[3];
     out[slice * V + v] = d;
   }
 }
@@ -3295,7 +3360,7 @@ struct Workspace {
   float* ba;
   float* rpart;
   float* dpart;
-  float* dsum;  // DP_PRE tile sums of DP_TE partials [slice][V]
+  float* dsum;  // DP_PRE: D of DP_QTE partials [slice][V]
   float* scal;
   float* tvc;
   float* tvn;
@@ -3336,8 +3401,8 @@ Workspace carve(char* base, int variant, int N, int E, int V, int M, int full) {
   w.I = (float*)take(S * M * 4);
   w.ba = (float*)take(S * M * 4);
   w.rpart = (float*)take(S * tiles * 4);
-  // DP_TE pads each (scenario, tile, row) epoch series to a multiple of 16
-  const size_t dp_te = (size_t)N * tiles * V * (size_t)dte_stride(E);
+  // DP_QTE pads each (scenario, quad, row) epoch series to a multiple of 16
+  const size_t dp_te = (size_t)N * yk::dp_quads((int)tiles) * V * (size_t)dte_stride(E);
   w.dpart = (float*)take(std::max(S * partial_tiles(variant, M) * V, dp_te) * 4);
   w.dsum = (float*)take(S * V * 4);
   w.scal = (float*)take(S * 8 * 4);
@@ -3530,11 +3595,10 @@ int launch_bonds_colnorm(RowCfg rc, hipStream_t st, yk::BondArgs& A, int* ptiles
 // in the engine c2 Yuma 3 bonds 1.66-1.72 -> 1.54-1.58 ms). Without the
 // history the same shapes lose (c2 1.05 -> 1.07-1.69 ms, c4 1.63 -> 1.63-1.84,
 // the c3 sweep 10.2 -> 10.6-14.7 ms: profiles/r03/ab/scan_shapes_nohist.txt).
-// Sweeps over one shared input trajectory run k_bonds_grp with K = 2
-// scenarios per block (K = 1 / 3 / 4 / 8 measured slower,
-// profiles/r03/ab/c3_scan_group_k.txt).
+// Sweeps over one shared input trajectory run k_bonds_grp with K = 4
+// scenarios per block (k_bonds_grp's history).
 constexpr int kWideP = 2;      // epochs in flight of the wide history scan
-constexpr int kScanGroup = 2;  // scenarios per block of the shared-input scan
+constexpr int kScanGroup = 4;  // scenarios per block of the shared-input scan
 int bonds_rows(bool vec, bool hist, bool wsh) { return vec && (hist || wsh) ? 2 : 1; }
 template <int VARIANT, int R, bool VEC, int P, bool VECI, bool NT, int BS, int CB, int DPL>
 int launch_elem_shape(hipStream_t st, yk::BondArgs& A) {
@@ -3550,7 +3614,7 @@ int launch_bonds_elem(hipStream_t st, yk::BondArgs& A) {
   const bool hist = A.B_hist != nullptr;
   if constexpr (VEC) {
     if (hist && A.M >= 1024)
-      return launch_elem_shape<VARIANT, 2, true, kWideP, true, true, 512, 1024, yk::DP_VT>(st, A);
+      return launch_elem_shape<VARIANT, 2, true, kWideP, true, true, 512, 1024, yk::DP_VQ>(st, A);
   }
   if constexpr (VEC) {
     if (A.wsh && A.N >= 2 && A.rq4 != nullptr) {  // a sweep over one input trajectory
@@ -3563,7 +3627,7 @@ int launch_bonds_elem(hipStream_t st, yk::BondArgs& A) {
     }
   }
   if (bonds_rows(VEC, hist, A.wsh != 0) != 2)
-    return launch_elem_shape<VARIANT, 1, VEC, 4, VEC, false, 256, 64, yk::DP_TE>(st, A);
+    return launch_elem_shape<VARIANT, 1, VEC, 4, VEC, false, 256, 256, yk::DP_QTE>(st, A);
   if (hist) return launch_elem_shape<VARIANT, 2, VEC, 2, VEC, true, 256, 64, yk::DP_TV>(st, A);
   return launch_elem_shape<VARIANT, 2, VEC, 2, VEC, false, 256, 64, yk::DP_TV>(st, A);
 }
@@ -3748,8 +3812,8 @@ int run_impl(int variant, const yuma_params_t* prm, int N, int E, int V, int M, 
                   : launch_bonds<false>(variant, rc, st, A, &ptiles);
     tm.mark(YUMA_PHASE_FINALIZE);
     const float* dsrc = ws.dpart;
-    if (dpl == yk::DP_TE) {
-      YK_LAUNCH(yk::k_dte_sum<false>, (long long)N * ((c1 - (c0 & ~15) + 15) / 16) * ((V + 3) / 4), 256, st,
+    if (dpl == yk::DP_QTE) {
+      YK_LAUNCH(yk::k_dte_sum, (long long)N * ((c1 - (c0 & ~15) + 15) / 16) * ((V + 3) / 4), 256, st,
                 ws.dpart, N, V, ptiles, A.ep, c0, c1, ws.dsum);
       dsrc = ws.dsum;
       dpl = yk::DP_PRE;
@@ -3868,8 +3932,8 @@ int shard_stage_impl(int stage, int variant, const yuma_params_t* prm, int N, in
                            out->Wn, out->Wc, ws.tvc, ws.tvn, 0);
       YK_LAUNCH(yk::k_rsum, ns, 64, st, ws.rpart, tiles, io->rsum_part);
       if (full) {
-        YK_LAUNCH(yk::k_dsum, ns, 256, st, ws.tvc, V, tiles, io->tv_part, (int)yk::DP_TV);
-        YK_LAUNCH(yk::k_dsum, ns, 256, st, ws.tvn, V, tiles, io->tv_part + ns * V, (int)yk::DP_TV);
+        YK_LAUNCH(yk::k_dsum, ns, 256, st, ws.tvc, V, tiles, io->tv_part);
+        YK_LAUNCH(yk::k_dsum, ns, 256, st, ws.tvn, V, tiles, io->tv_part + ns * V);
       }
       break;
     }
@@ -3909,11 +3973,11 @@ int shard_stage_impl(int stage, int variant, const yuma_params_t* prm, int N, in
       int ptiles = tiles;
       const int dpl = vec ? launch_bonds<true>(variant, rc, st, A, &ptiles)
                           : launch_bonds<false>(variant, rc, st, A, &ptiles);
-      if (dpl == yk::DP_TE)
-        YK_LAUNCH(yk::k_dte_sum<true>, (long long)N * ((E + 15) / 16) * ((V + 15) / 16), 256, st, ws.dpart, N,
-                  V, ptiles, A.ep, 0, E, io->dsum_part);
+      if (dpl == yk::DP_QTE)
+        YK_LAUNCH(yk::k_dte_sum, (long long)N * ((E + 15) / 16) * ((V + 3) / 4), 256, st, ws.dpart, N, V,
+                  ptiles, A.ep, 0, E, io->dsum_part);
       else
-        YK_LAUNCH(yk::k_dsum, ns, 256, st, ws.dpart, V, ptiles, io->dsum_part, dpl);
+        YK_LAUNCH(yk::k_dsum_canon, ns, 256, st, ws.dpart, V, ptiles, io->dsum_part, dpl);
       break;
     }
     case 5: {
