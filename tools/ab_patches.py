@@ -145,3 +145,9 @@ PATCHES["wc_a"] = PATCHES["elem_uncond"] + [_NOHIST]
 PATCHES["wc_b"] = PATCHES["elem_uncond"] + [_NOTE]
 PATCHES["wc_c"] = PATCHES["elem_uncond"] + [_NORESET]
 PATCHES["wc_d"] = PATCHES["elem_uncond"] + [_NOHIST, _NOTE, _NORESET]
+# k_consensus_p: non-temporal W loads (whole lines per wave now); 3 waves / SIMD
+_CP_LOAD = "      const float4 t = *reinterpret_cast<const float4*>(Ws + (o0 + (unsigned)i * st));\n      wn[i][0] = t.x;\n      wn[i][1] = t.y;\n      wn[i][2] = t.z;\n      wn[i][3] = t.w;\n    }\n  } else {\n#pragma unroll\n    for (int i = 0; i < R; ++i) load4c<VEC>(Ws, r0 + 8 * i, V, m, M, wn[i]);"
+PATCHES["cp_ntl"] = [(_CP_LOAD, _CP_LOAD.replace("const float4 t = *reinterpret_cast<const float4*>(Ws + (o0 + (unsigned)i * st));",
+                                                  "const fvec4 t = __builtin_nontemporal_load(reinterpret_cast<const fvec4*>(Ws + (o0 + (unsigned)i * st)));"))]
+PATCHES["cp_w3"] = [("__global__ __launch_bounds__(256, 4) void k_consensus_p(", "__global__ __launch_bounds__(256, 3) void k_consensus_p(")]
+PATCHES["cp_ntl_w3"] = PATCHES["cp_ntl"] + PATCHES["cp_w3"]

@@ -1275,6 +1275,393 @@ __global__ __launch_bounds__(256, 4) void k_consensus_w(const float* __restrict_
       if (m + c < M) craw[slice * M + m + c] = (double)hi_k[c] / (double)top;
 }
 
+// ---------------------------------------------------------------------------
+// Consensus with 128-byte row segments (round 4). Same
+// block / tile as k_consensus_w (one 64-miner tile of one slice), but two
+// waves share each 32-miner column group: pair p = wave / 2 owns miners
+// 32p .. 32p+31 of the tile, half h = wave % 2 the rows 128h + rg + 8i, and
+// lane (cq, rg) = (lane / 8, lane % 8) holds rows rg + 8i of the columns
+// 4cq .. 4cq+3. A wave load moves 8 rows x 128 B -- whole lines -- instead of
+// k_consensus_w's 16 rows x 64 B, whose line halves land in two waves.
+// Column reductions: the 8-lane DPP butterfly inside the wave, then the two
+// halves of the pair through LDS, always added h0 + h1, so both waves of a
+// pair hold the same bits. Every exchange is one block barrier, so the search
+// steps are block-uniform: a narrowing / bisection pass runs while any wave
+// of the block has an active column (flags exchanged with the partials), and
+// the histogram-or-bisection finish is decided for the block. The histogram
+// is shared by the pair (integer atomics: any order), zeroed ahead of the
+// bracket barrier. W loads are non-temporal (whole lines per wave now; in
+// k_consensus_w, whose line halves go to two waves, they lost). 3 waves /
+// SIMD: at 4 (128 VGPRs) 3 VGPRs spilled, consensus 0.95 ms against 0.86.
+// Measured at c2 (profiles/r04/ab_round6.txt): 0.852-0.853 ms against
+// 0.869 for k_consensus_w. V in (64, 256].
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float wsum8(float x) {
+  x = x + dpp_f<0xB1>(x);   // quad_perm [1,0,3,2]
+  x = x + dpp_f<0x4E>(x);   // quad_perm [2,3,0,1]
+  x = x + dpp_f<0x141>(x);  // row_half_mirror: lane i <-> 7 - i of each 8-lane half
+  return x;
+}
+__device__ __forceinline__ int iwsum8(int x) {
+  x = x + __builtin_amdgcn_mov_dpp(x, 0xB1, 0xF, 0xF, false);
+  x = x + __builtin_amdgcn_mov_dpp(x, 0x4E, 0xF, 0xF, false);
+  x = x + __builtin_amdgcn_mov_dpp(x, 0x141, 0xF, 0xF, false);
+  return x;
+}
+__device__ __forceinline__ int iwmax8(int x) {
+  x = max(x, __builtin_amdgcn_mov_dpp(x, 0xB1, 0xF, 0xF, false));
+  x = max(x, __builtin_amdgcn_mov_dpp(x, 0x4E, 0xF, 0xF, false));
+  x = max(x, __builtin_amdgcn_mov_dpp(x, 0x141, 0xF, 0xF, false));
+  return x;
+}
+__device__ __forceinline__ int iwmin8(int x) {
+  x = min(x, __builtin_amdgcn_mov_dpp(x, 0xB1, 0xF, 0xF, false));
+  x = min(x, __builtin_amdgcn_mov_dpp(x, 0x4E, 0xF, 0xF, false));
+  x = min(x, __builtin_amdgcn_mov_dpp(x, 0x141, 0xF, 0xF, false));
+  return x;
+}
+// exclusive prefix sum over the 8 lanes of a half row (row_shr with
+// bound_ctrl; shifts that cross into the other half are masked)
+__device__ __forceinline__ int iscan8_excl(int x, int r8) {
+  int y = x;
+  int t = __builtin_amdgcn_update_dpp(0, y, 0x111, 0xF, 0xF, true);
+  y = y + (r8 >= 1 ? t : 0);
+  t = __builtin_amdgcn_update_dpp(0, y, 0x112, 0xF, 0xF, true);
+  y = y + (r8 >= 2 ? t : 0);
+  t = __builtin_amdgcn_update_dpp(0, y, 0x114, 0xF, 0xF, true);
+  y = y + (r8 >= 4 ? t : 0);
+  return y - x;
+}
+
+template <bool VEC>
+__global__ __launch_bounds__(256, 3) void k_consensus_p(const float* __restrict__ W,
+                                                     const float* __restrict__ rsd,
+                                                     const float* __restrict__ sn,
+                                                     const int* __restrict__ sx,
+                                                     const yuma_params_t* __restrict__ prm, int N,
+                                                     int V, int M, long long slice0, int tiles,
+                                                     double* __restrict__ craw,
+                                                     float* __restrict__ Pout, int wsh,
+                                                     const int* __restrict__ crep) {
+  constexpr int R = 16, HR = 8 * R;  // rows per lane, rows per half
+  __shared__ __attribute__((aligned(16))) unsigned hb[2 * 32 * kHS];  // per pair: 32 columns
+  __shared__ __attribute__((aligned(16))) float rl[4][3 * HR];        // per wave: sums, stakes, 1 / sums
+  __shared__ float xf[2][4][32];  // float exchange, double-buffered
+  __shared__ int xi[2][4][32];    // bracket max / min bit patterns
+  __shared__ unsigned xflag[2][4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int pair = wave >> 1, h = wave & 1, pw = wave ^ 1;
+  const int cq = lane >> 3, rg = lane & 7;
+  const long long slice = slice0 + blockIdx.x / tiles;
+  const int tile = blockIdx.x % tiles;
+  const int n = (int)(slice % N);
+  if (dup_slice(crep, slice, N)) return;  // block-uniform
+  const int m = tile * kTileM + pair * 32 + cq * 4;
+  const int r0 = h * HR + rg;  // this lane's rows r0 + 8 i
+  const float* Ws = W + in_slice(slice, N, wsh) * (long long)V * M;
+  const float* rsd_s = rsd + slice * V;
+  const float* sn_s = sn + slice * V;
+  float* rw = rl[wave];
+
+  // load + normalise (load_norm_w_lds over the half's rows)
+  float dv[2], sv[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int jj = min(h * HR + lane + 64 * k, V - 1);
+    dv[k] = rsd_s[jj];
+    sv[k] = sn_s[jj];
+  }
+  float wn[R][4];
+  const bool full = r0 + 8 * (R - 1) < V && m + 3 < M;
+  const bool allfull = VEC && __all(full) && (long long)V * M < (1ll << 30);
+  if (allfull) {
+    const unsigned o0 = (unsigned)r0 * (unsigned)M + (unsigned)m, st = 8u * (unsigned)M;
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const fvec4 t = __builtin_nontemporal_load(reinterpret_cast<const fvec4*>(Ws + (o0 + (unsigned)i * st)));
+      wn[i][0] = t.x;
+      wn[i][1] = t.y;
+      wn[i][2] = t.z;
+      wn[i][3] = t.w;
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < R; ++i) load4c<VEC>(Ws, r0 + 8 * i, V, m, M, wn[i]);
+  }
+  float amax = 0.0f, dmin = INFINITY;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int j = lane + 64 * k;
+    amax = fmaxf(amax, fabsf(dv[k]));
+    dmin = fminf(dmin, fabsf(dv[k]));
+    rw[j] = dv[k];
+    rw[HR + j] = h * HR + j < V ? sv[k] : 0.0f;
+    rw[2 * HR + j] = 1.0f / dv[k];
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  {
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    unsigned ymin = 0xFFFFFFFFu;
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const float d = rw[rg + 8 * i];
+      const float r = rw[2 * HR + rg + 8 * i];
+      const f2 r2 = {r, r}, nd2 = {-d, -d};
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        const f2 a2 = {wn[i][2 * hh], wn[i][2 * hh + 1]};
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          amax = fmaxf(amax, fabsf(a2[c]));
+          const unsigned y = (__float_as_uint(a2[c]) << 1) - 1u;
+          ymin = y < ymin ? y : ymin;
+        }
+        const f2 q = a2 * r2;
+        const f2 e = __builtin_elementwise_fma(nd2, q, a2);
+        const f2 q1 = __builtin_elementwise_fma(e, r2, q);
+        wn[i][2 * hh] = q1[0];
+        wn[i][2 * hh + 1] = q1[1];
+      }
+    }
+    const bool slow = !(dmin >= 0x1p-60f && amax <= 0x1p60f &&
+                        (ymin == 0xFFFFFFFFu || ymin + 1u >= (__float_as_uint(0x1p-60f) << 1)));
+    if (__any(slow)) {  // rare: some operand outside the fast-division guard
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        load4c<VEC>(Ws, r0 + 8 * i, V, m, M, wn[i]);
+        const float d = rw[rg + 8 * i];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) wn[i][c] = wn[i][c] / d;
+      }
+    }
+    if (!__all(full)) {
+#pragma unroll
+      for (int i = 0; i < R; ++i) mask4(r0 + 8 * i, V, m, M, wn[i]);
+    }
+  }
+  const int col = cq * 4;  // this lane's first column within the pair's 32
+  // stakes are read from LDS at every use (an empty asm on the offset keeps
+  // the compiler from hoisting the 16 reads into registers)
+  auto stake_off = [&]() {
+    int off = HR + rg;
+    asm volatile("" : "+v"(off));
+    return off;
+  };
+
+  if (Pout != nullptr) {  // P = sum_v S·Wn (yumas.py:192)
+    float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    const int so = stake_off();
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const float si = rw[so + 8 * i];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) acc[c] = acc[c] + si * wn[i][c];
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc[c] = wsum8(acc[c]);
+    if (rg == 0)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) xf[1][wave][col + c] = acc[c];
+    lds_barrier();
+    if (h == 0 && rg == 0)
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        if (m + c < M) Pout[slice * M + m + c] = xf[1][wave][col + c] + xf[1][pw][col + c];
+    lds_barrier();
+  }
+
+  const yuma_params_t& p = prm[n];
+  const float kappa = p.kappa;
+  const int top = 1 << p.bisect_iters;
+  const float scale = (float)top, inv_scale = 1.0f / scale;
+  // bracket (consensus_search): column max / min of the bit patterns, stake total
+  int lo_k[4], hi_k[4];
+  {
+    bool odd = false;
+    float stot = 0.0f;
+    int imax[4], imin[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      imax[c] = INT_MIN;
+      imin[c] = INT_MAX;
+    }
+    const int so = stake_off();
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const float si = rw[so + 8 * i];
+      odd |= !(si >= 0.0f) || si == INFINITY;
+      stot = stot + si;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int b = __float_as_int(wn[i][c]);
+        imax[c] = b > imax[c] ? b : imax[c];
+        imin[c] = b < imin[c] ? b : imin[c];
+      }
+    }
+    stot = wsum8(stot);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      imax[c] = iwmax8(imax[c]);
+      imin[c] = iwmin8(imin[c]);
+    }
+    const bool odd_w = __any(odd);
+    {  // zero the pair's histogram ahead of the bracket barrier (used only after it)
+      uint4* hz = reinterpret_cast<uint4*>(hb + pair * 32 * kHS);
+      constexpr int NW4 = 32 * kHS / 4;
+      for (int j = h * (NW4 / 2) + lane; j < (h + 1) * (NW4 / 2); j += 64) hz[j] = make_uint4(0u, 0u, 0u, 0u);
+    }
+    if (rg == 0)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        xi[0][wave][col + c] = imax[c];
+        xi[1][wave][col + c] = imin[c];
+      }
+    if (lane == 0) {
+      xf[0][wave][0] = stot;
+      xflag[0][wave] = odd_w ? 1u : 0u;
+    }
+    lds_barrier();
+    // both pairs hold the same rows: block-uniform
+    const bool bracket = !(xflag[0][wave] | xflag[0][pw]) && kappa >= 0.0f;
+    const float stot_p = xf[0][pair * 2][0] + xf[0][pair * 2 + 1][0];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      lo_k[c] = 0;
+      hi_k[c] = top;
+      if (!bracket) continue;
+      const int mx = max(xi[0][wave][col + c], xi[0][pw][col + c]);
+      const int mn = min(xi[1][wave][col + c], xi[1][pw][col + c]);
+      const bool nanc = mx > 0x7f800000;
+      const float vmx = __int_as_float(mx);
+      const float vmn = mn > 0 ? __int_as_float(mn) : 0.0f;
+      const int gmax = vmx > 0.0f ? (int)fminf(ceilf(vmx * scale), scale) : 0;
+      const int gmin = vmn > 0.0f ? (int)fminf(ceilf(vmn * scale), scale + 1.0f) : 0;
+      int lo_c = gmin >= 2 ? gmin - 1 : 0;
+      int hi_c = gmax < 1 ? 1 : gmax;
+      if (lo_c > 0 && !(stot_p > kappa)) {
+        lo_c = 0;
+        hi_c = 1;
+      }
+      if (lo_c >= top) {
+        lo_c = top - 1;
+        hi_c = top;
+      }
+      if (hi_c <= lo_c) hi_c = lo_c + 1;
+      lo_k[c] = nanc ? 0 : lo_c;
+      hi_k[c] = nanc ? top : hi_c;
+    }
+    // passes: narrowing to <= kHB - 1 grid points (exact stakes), else
+    // bisection to width 1; block-uniform pass count (flags with the partials)
+    bool hist = bracket && (p.flags & YUMA_FLAG_NO_HIST) == 0 && sx[slice] >= 0;
+    int lim = hist ? kHB - 1 : 1;
+    int buf = 1;
+    bool wide_block = false;
+    for (;;) {
+      for (;;) {
+        bool active = false, wide = false;
+        float part[4], midf[4];
+        int mid[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          active |= (hi_k[c] - lo_k[c]) > lim;
+          wide |= (hi_k[c] - lo_k[c]) > kHistMinW;
+          mid[c] = (lo_k[c] + hi_k[c]) >> 1;
+          midf[c] = (float)mid[c] * inv_scale;
+          part[c] = 0.0f;
+        }
+        const unsigned fl = (__any(active) ? 1u : 0u) | (__any(wide) ? 2u : 0u);
+        if (fl & 1u) {  // wave-uniform: a wave with no active column skips the sums
+          const int so2 = stake_off();
+#pragma unroll
+          for (int i = 0; i < R; ++i) {
+            const float si = rw[so2 + 8 * i];
+            const float zs = 0.0f * si;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) part[c] = part[c] + ((wn[i][c] > midf[c]) ? si : zs);
+          }
+#pragma unroll
+          for (int c = 0; c < 4; ++c) part[c] = wsum8(part[c]);
+          if (rg == 0)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) xf[buf][wave][col + c] = part[c];
+        }
+        if (lane == 0) xflag[buf][wave] = fl;
+        lds_barrier();
+        const unsigned all = xflag[buf][0] | xflag[buf][1] | xflag[buf][2] | xflag[buf][3];
+        // the pair's two halves have the same columns, hence the same flags
+        if ((all & 1u) == 0) {
+          wide_block = (all & 2u) != 0;
+          buf ^= 1;
+          break;
+        }
+        if (fl & 1u) {
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            const float f = xf[buf][pair * 2][col + c] + xf[buf][pair * 2 + 1][col + c];
+            const bool act = hi_k[c] - lo_k[c] > lim, up = f > kappa;
+            lo_k[c] = (act && up) ? mid[c] : lo_k[c];
+            hi_k[c] = (act && !up) ? mid[c] : hi_k[c];
+          }
+        }
+        buf ^= 1;
+      }
+      if (!hist || wide_block) break;
+      hist = false;  // narrow brackets (a wide subnet): bisection finish
+      lim = 1;
+    }
+    if (hist) {
+      // exact-stake histogram finish (consensus_search), shared by the pair
+      const double kd = floor((double)kappa * 16777216.0);
+      const int thr = sx[slice] - (kd > 33554432.0 ? 33554432 : (int)kd);
+      unsigned* hp = hb + pair * 32 * kHS;  // zeroed before the bracket barrier
+      float nlo[4];
+      unsigned w[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        nlo[c] = -(float)lo_k[c];
+        w[c] = (unsigned)(hi_k[c] - lo_k[c]);
+      }
+      const int so = stake_off();
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        const unsigned su = (unsigned)(rw[so + 8 * i] * 16777216.0f);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const unsigned k = (unsigned)ceilf(fmaf(wn[i][c], scale, nlo[c]));
+          atomicAdd(hp + (col + c) * kHS + (k < w[c] ? k : w[c]), su);
+        }
+      }
+      lds_barrier();
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const unsigned* hc = hp + (col + c) * kHS + 8 * rg;
+        const uint4 a = *reinterpret_cast<const uint4*>(hc);
+        const uint4 b = *reinterpret_cast<const uint4*>(hc + 4);
+        int q[8];
+        q[0] = (int)a.x;
+        q[1] = q[0] + (int)a.y;
+        q[2] = q[1] + (int)a.z;
+        q[3] = q[2] + (int)a.w;
+        q[4] = q[3] + (int)b.x;
+        q[5] = q[4] + (int)b.y;
+        q[6] = q[5] + (int)b.z;
+        q[7] = q[6] + (int)b.w;
+        const int t = thr - iscan8_excl(q[7], rg);
+        int cnt = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) cnt += q[j] < t ? 1 : 0;
+        hi_k[c] = lo_k[c] + max(iwsum8(cnt), 1);
+      }
+    }
+  }
+  if (h == 0 && rg == 0)
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      if (m + c < M) craw[slice * M + m + c] = (double)hi_k[c] / (double)top;
+}
+
 // Clip + rank (yumas.py:214-217; Yuma2 clips W_prev :328), wave-owned columns.
 // rpart[slice][tile] = sum over the tile's 64 miners (wave sums, waves in order).
 template <int R, bool VEC, bool YUMA2, bool FULL>
@@ -3453,9 +3840,13 @@ void launch_consensus(RowCfg rc, long long nblocks, hipStream_t st, const float*
       launch_consensus_w<4, VEC>(nblocks, st, W, rsd, sn, sx, prm, N, V, M, slice0, tiles, craw,
                                   P, wsh, crep);
       return;
-    case RC_256_16:
-      launch_consensus_w<16, VEC>(nblocks, st, W, rsd, sn, sx, prm, N, V, M, slice0, tiles, craw,
-                                  P, wsh, crep);
+    case RC_256_16:  // 65-256 validators: 128-byte row segments, wave pairs (float4 rows)
+      if constexpr (VEC)
+        YK_LAUNCH((yk::k_consensus_p<true>), nblocks, 256, st, W, rsd, sn, sx, prm, N, V, M, slice0, tiles,
+                  craw, P, wsh, crep);
+      else
+        launch_consensus_w<16, false>(nblocks, st, W, rsd, sn, sx, prm, N, V, M, slice0, tiles, craw, P, wsh,
+                                      crep);
       return;
     default:
       break;
