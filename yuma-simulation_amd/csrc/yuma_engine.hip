@@ -2986,7 +2986,14 @@ __global__ __launch_bounds__(BS, 1) void k_bonds_elem(BondArgs A) {
   }
 
   float rw[P][R][4], rd[P][R], rsn[P][R], ri[P][4], rba[P][4];
-  float gq[R];  // DP_QTE: lane j < 16 holds the quad partial of epoch (t & ~15) + j
+  // DP_QTE: the quad partials of up to kQBuf epochs parked in LDS (one float
+  // per wave row and epoch) and written out as contiguous runs when the
+  // buffer fills or the launch ends: no global store inside the epoch loop
+  // (partial stores cost the read stream far more than their bytes:
+  // [slice][tile][V] stores 0.24 ms at c4, 16-epoch 64-byte runs still 0.16)
+  constexpr int kQBuf = 256, NWB = BS / 64;
+  __shared__ float qbuf[DPL == DP_QTE ? NWB * R * kQBuf : 1];
+  int tq = A.t0;  // first epoch held in qbuf
   auto fetch = [&](int k, int t) {
     const long long slice = (long long)t * N + n;
 #pragma unroll
@@ -3117,13 +3124,19 @@ __global__ __launch_bounds__(BS, 1) void k_bonds_elem(BondArgs A) {
           q = q + __shfl_xor(q, 32, 64);
           const int quad = m >> 8, nq = dp_quads(A.tiles);
           if constexpr (DPL == DP_QTE) {
-            // (the [slice][tile][V] 4-byte stores cost this scan 0.24 ms at
-            // c4: timing-only build without them, 1.50 -> 1.26 ms)
-            if (lane == (t & 15)) gq[i] = q;
-            if ((t & 15) == 15 || t == A.t1 - 1) {
-              const int te = (t & ~15) + lane;
-              if (lane < 16 && te >= A.t0 && te <= t && row < V && quad < nq)
-                A.dpart[((long long)(n * nq + quad) * V + row) * A.ep + te] = gq[i];
+            float* qb = qbuf + ((threadIdx.x >> 6) * R + i) * kQBuf;
+            if (lane == 0) qb[t - tq] = q;
+            if (t - tq == kQBuf - 1 || t == A.t1 - 1) {  // wave-uniform
+              __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+              __builtin_amdgcn_wave_barrier();
+              __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+              float* dq = A.dpart + ((long long)(n * nq + quad) * V + row) * A.ep + tq;
+              if (row < V && quad < nq)
+                for (int e = lane; e <= t - tq; e += 64) dq[e] = qb[e];
+              __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+              __builtin_amdgcn_wave_barrier();
+              __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+              if (i == R - 1) tq = t + 1;
             }
           } else if (lane == 0 && row < V && quad < nq) {
             A.dpart[(slice * V + row) * (long long)nq + quad] = q;
