@@ -1291,7 +1291,8 @@ __global__ __launch_bounds__(256, 4) void k_consensus_w(const float* __restrict_
 // the histogram-or-bisection finish is decided for the block. The histogram
 // is shared by the pair (integer atomics: any order), zeroed ahead of the
 // bracket barrier. W loads are non-temporal (whole lines per wave now; in
-// k_consensus_w, whose line halves go to two waves, they lost). 3 waves /
+// k_consensus_w, whose line halves go to two waves, they lost). Not used for
+// shared-input sweeps (launch_consensus). 3 waves /
 // SIMD: at 4 (128 VGPRs) 3 VGPRs spilled, consensus 0.95 ms against 0.86.
 // Measured at c2 (profiles/r04/ab_round6.txt): 0.852-0.853 ms against
 // 0.869 for k_consensus_w. V in (64, 256].
@@ -3854,12 +3855,16 @@ void launch_consensus(RowCfg rc, long long nblocks, hipStream_t st, const float*
                                   P, wsh, crep);
       return;
     case RC_256_16:  // 65-256 validators: 128-byte row segments, wave pairs (float4 rows)
-      if constexpr (VEC)
+      // shared-input sweeps keep the wave-owned kernel: there the consensus
+      // classes re-read each slice from the Infinity Cache and the pairs'
+      // barriers are what shows (c3 0.70 ms against 0.85-0.86 with or
+      // without the non-temporal loads)
+      if (VEC && !wsh)
         YK_LAUNCH((yk::k_consensus_p<true>), nblocks, 256, st, W, rsd, sn, sx, prm, N, V, M, slice0, tiles,
                   craw, P, wsh, crep);
       else
-        launch_consensus_w<16, false>(nblocks, st, W, rsd, sn, sx, prm, N, V, M, slice0, tiles, craw, P, wsh,
-                                      crep);
+        launch_consensus_w<16, VEC>(nblocks, st, W, rsd, sn, sx, prm, N, V, M, slice0, tiles, craw, P, wsh,
+                                    crep);
       return;
     default:
       break;
