@@ -106,7 +106,7 @@ def kernel_of(phase: str, variant: int, shared: bool = False, V: int = 256, M: i
             return "k_bonds_grp" if shared and N > 1 else "k_bonds_elem"
         return "k_bonds_cn" if V > 64 and M % 4 == 0 else "k_bonds"
     if phase == "consensus" and 64 < V <= 256 and M % 4 == 0 and not shared:
-        return "k_consensus_p"  # 128-byte row segments (wave pairs)
+        return "k_consensus_p"  # 128-byte row segments (wave pairs; run outputs)
     return PHASE_KERNELS[phase]
 
 

@@ -3858,8 +3858,13 @@ void launch_consensus(RowCfg rc, long long nblocks, hipStream_t st, const float*
       // shared-input sweeps keep the wave-owned kernel: there the consensus
       // classes re-read each slice from the Infinity Cache and the pairs'
       // barriers are what shows (c3 0.70 ms against 0.85-0.86 with or
-      // without the non-temporal loads)
-      if (VEC && !wsh)
+      // without the non-temporal loads). So do runs that ask for the prerank
+      // P (full outputs): its sum order is the wave-owned kernel's, the same
+      // bits in a sweep and in the replicated run. C does not depend on the
+      // kernel for exact-stake inputs (the histogram / bisection sums are
+      // exact); for generic float stakes the two kernels' F sums may differ
+      // in the last bit at a tie, inside the tie window the tests allow.
+      if (VEC && !wsh && P == nullptr)
         YK_LAUNCH((yk::k_consensus_p<true>), nblocks, 256, st, W, rsd, sn, sx, prm, N, V, M, slice0, tiles,
                   craw, P, wsh, crep);
       else
