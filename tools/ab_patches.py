@@ -151,3 +151,10 @@ PATCHES["cp_ntl"] = [(_CP_LOAD, _CP_LOAD.replace("const float4 t = *reinterpret_
                                                   "const fvec4 t = __builtin_nontemporal_load(reinterpret_cast<const fvec4*>(Ws + (o0 + (unsigned)i * st)));"))]
 PATCHES["cp_w3"] = [("__global__ __launch_bounds__(256, 4) void k_consensus_p(", "__global__ __launch_bounds__(256, 3) void k_consensus_p(")]
 PATCHES["cp_ntl_w3"] = PATCHES["cp_ntl"] + PATCHES["cp_w3"]
+# history-less scan: 2-row blocks (twice the blocks: c2 has 1024 4-row blocks, one dispatch round)
+PATCHES["qte_bs128"] = [("    return launch_elem_shape<VARIANT, 1, VEC, 4, VEC, false, 256, 256, yk::DP_QTE>(st, A);",
+                         "    return launch_elem_shape<VARIANT, 1, VEC, 4, VEC, false, 128, 256, yk::DP_QTE>(st, A);")]
+PATCHES["qte_bs128_p6"] = [("    return launch_elem_shape<VARIANT, 1, VEC, 4, VEC, false, 256, 256, yk::DP_QTE>(st, A);",
+                            "    return launch_elem_shape<VARIANT, 1, VEC, 6, VEC, false, 128, 256, yk::DP_QTE>(st, A);")]
+PATCHES["qte_p6"] = [("    return launch_elem_shape<VARIANT, 1, VEC, 4, VEC, false, 256, 256, yk::DP_QTE>(st, A);",
+                      "    return launch_elem_shape<VARIANT, 1, VEC, 6, VEC, false, 256, 256, yk::DP_QTE>(st, A);")]

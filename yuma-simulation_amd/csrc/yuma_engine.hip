@@ -1286,9 +1286,9 @@ __global__ __launch_bounds__(256, 4) void k_consensus_w(const float* __restrict_
 // Column reductions: the 8-lane DPP butterfly inside the wave, then the two
 // halves of the pair through LDS, always added h0 + h1, so both waves of a
 // pair hold the same bits. Every exchange is one block barrier, so the search
-// steps are block-uniform: a narrowing / bisection pass runs while any wave
-// of the block has an active column (flags exchanged with the partials), and
-// the histogram-or-bisection finish is decided for the block. The histogram
+// steps are block-uniform: every wave reads all four waves' bracket data from
+// the bracket exchange, derives the block's widest bracket and from it the
+// pass count and the histogram-or-bisection finish. The histogram
 // is shared by the pair (integer atomics: any order), zeroed ahead of the
 // bracket barrier. W loads are non-temporal (whole lines per wave now; in
 // k_consensus_w, whose line halves go to two waves, they lost). Not used for
@@ -1526,14 +1526,12 @@ __global__ __launch_bounds__(256, 3) void k_consensus_p(const float* __restrict_
     lds_barrier();
     // both pairs hold the same rows: block-uniform
     const bool bracket = !(xflag[0][wave] | xflag[0][pw]) && kappa >= 0.0f;
-    const float stot_p = xf[0][pair * 2][0] + xf[0][pair * 2 + 1][0];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      lo_k[c] = 0;
-      hi_k[c] = top;
-      if (!bracket) continue;
-      const int mx = max(xi[0][wave][col + c], xi[0][pw][col + c]);
-      const int mn = min(xi[1][wave][col + c], xi[1][pw][col + c]);
+    // a column's bracket from the block's exchanged max / min bit patterns
+    // and its pair's stake total (consensus_search's rules)
+    auto bracket_of = [&](int mx, int mn, float st, int& lo, int& hi) {
+      lo = 0;
+      hi = top;
+      if (!bracket) return;
       const bool nanc = mx > 0x7f800000;
       const float vmx = __int_as_float(mx);
       const float vmn = mn > 0 ? __int_as_float(mn) : 0.0f;
@@ -1541,7 +1539,7 @@ __global__ __launch_bounds__(256, 3) void k_consensus_p(const float* __restrict_
       const int gmin = vmn > 0.0f ? (int)fminf(ceilf(vmn * scale), scale + 1.0f) : 0;
       int lo_c = gmin >= 2 ? gmin - 1 : 0;
       int hi_c = gmax < 1 ? 1 : gmax;
-      if (lo_c > 0 && !(stot_p > kappa)) {
+      if (lo_c > 0 && !(st > kappa)) {
         lo_c = 0;
         hi_c = 1;
       }
@@ -1550,67 +1548,77 @@ __global__ __launch_bounds__(256, 3) void k_consensus_p(const float* __restrict_
         hi_c = top;
       }
       if (hi_c <= lo_c) hi_c = lo_c + 1;
-      lo_k[c] = nanc ? 0 : lo_c;
-      hi_k[c] = nanc ? top : hi_c;
+      lo = nanc ? 0 : lo_c;
+      hi = nanc ? top : hi_c;
+    };
+    const float stot_p = xf[0][pair * 2][0] + xf[0][pair * 2 + 1][0];
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      bracket_of(max(xi[0][wave][col + c], xi[0][pw][col + c]), min(xi[1][wave][col + c], xi[1][pw][col + c]),
+                 stot_p, lo_k[c], hi_k[c]);
+    // the widest bracket of the BLOCK, from the same exchange (lane l forms
+    // column l's bracket): every wave derives the same pass schedule, so the
+    // search needs no activity flags and no closing all-idle pass
+    int wmax;
+    {
+      const int pl = lane >> 5, cl = lane & 31;
+      int lo, hi;
+      bracket_of(max(xi[0][2 * pl][cl], xi[0][2 * pl + 1][cl]), min(xi[1][2 * pl][cl], xi[1][2 * pl + 1][cl]),
+                 xf[0][2 * pl][0] + xf[0][2 * pl + 1][0], lo, hi);
+      wmax = iwmax16(hi - lo);
+      wmax = max(wmax, __shfl_xor(wmax, 16, 64));
+      wmax = max(wmax, __shfl_xor(wmax, 32, 64));
     }
-    // passes: narrowing to <= kHB - 1 grid points (exact stakes), else
-    // bisection to width 1; block-uniform pass count (flags with the partials)
-    bool hist = bracket && (p.flags & YUMA_FLAG_NO_HIST) == 0 && sx[slice] >= 0;
-    int lim = hist ? kHB - 1 : 1;
+    // passes (each halves every active bracket to at most ceil(w / 2)):
+    // exact stakes and some bracket wider than kHistMinW -> narrow to
+    // <= kHB - 1 grid points, then the histogram; otherwise bisect to width 1
+    // (the histogram finish equals the bisection, so deciding on the block's
+    // widest initial bracket gives the same result)
+    bool hist = bracket && (p.flags & YUMA_FLAG_NO_HIST) == 0 && sx[slice] >= 0 && wmax > kHistMinW;
+    const int lim = hist ? kHB - 1 : 1;
+    int npass = 0;
+    for (int w = wmax; w > lim; w = (w + 1) >> 1) ++npass;
     int buf = 1;
-    bool wide_block = false;
-    for (;;) {
-      for (;;) {
-        bool active = false, wide = false;
-        float part[4], midf[4];
-        int mid[4];
+    for (int ps = 0; ps < npass; ++ps) {
+      bool active = false;
+      float part[4], midf[4];
+      int mid[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        active |= (hi_k[c] - lo_k[c]) > lim;
+        mid[c] = (lo_k[c] + hi_k[c]) >> 1;
+        midf[c] = (float)mid[c] * inv_scale;
+        part[c] = 0.0f;
+      }
+      // the pair's two waves hold the same brackets: a wave with no active
+      // column (and its partner) skips the sums, never the barrier
+      const bool wact = __any(active);
+      if (wact) {
+        const int so2 = stake_off();
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+          const float si = rw[so2 + 8 * i];
+          const float zs = 0.0f * si;
+#pragma unroll
+          for (int c = 0; c < 4; ++c) part[c] = part[c] + ((wn[i][c] > midf[c]) ? si : zs);
+        }
+#pragma unroll
+        for (int c = 0; c < 4; ++c) part[c] = wsum8(part[c]);
+        if (rg == 0)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) xf[buf][wave][col + c] = part[c];
+      }
+      lds_barrier();
+      if (wact) {
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
-          active |= (hi_k[c] - lo_k[c]) > lim;
-          wide |= (hi_k[c] - lo_k[c]) > kHistMinW;
-          mid[c] = (lo_k[c] + hi_k[c]) >> 1;
-          midf[c] = (float)mid[c] * inv_scale;
-          part[c] = 0.0f;
+          const float f = xf[buf][pair * 2][col + c] + xf[buf][pair * 2 + 1][col + c];
+          const bool act = hi_k[c] - lo_k[c] > lim, up = f > kappa;
+          lo_k[c] = (act && up) ? mid[c] : lo_k[c];
+          hi_k[c] = (act && !up) ? mid[c] : hi_k[c];
         }
-        const unsigned fl = (__any(active) ? 1u : 0u) | (__any(wide) ? 2u : 0u);
-        if (fl & 1u) {  // wave-uniform: a wave with no active column skips the sums
-          const int so2 = stake_off();
-#pragma unroll
-          for (int i = 0; i < R; ++i) {
-            const float si = rw[so2 + 8 * i];
-            const float zs = 0.0f * si;
-#pragma unroll
-            for (int c = 0; c < 4; ++c) part[c] = part[c] + ((wn[i][c] > midf[c]) ? si : zs);
-          }
-#pragma unroll
-          for (int c = 0; c < 4; ++c) part[c] = wsum8(part[c]);
-          if (rg == 0)
-#pragma unroll
-            for (int c = 0; c < 4; ++c) xf[buf][wave][col + c] = part[c];
-        }
-        if (lane == 0) xflag[buf][wave] = fl;
-        lds_barrier();
-        const unsigned all = xflag[buf][0] | xflag[buf][1] | xflag[buf][2] | xflag[buf][3];
-        // the pair's two halves have the same columns, hence the same flags
-        if ((all & 1u) == 0) {
-          wide_block = (all & 2u) != 0;
-          buf ^= 1;
-          break;
-        }
-        if (fl & 1u) {
-#pragma unroll
-          for (int c = 0; c < 4; ++c) {
-            const float f = xf[buf][pair * 2][col + c] + xf[buf][pair * 2 + 1][col + c];
-            const bool act = hi_k[c] - lo_k[c] > lim, up = f > kappa;
-            lo_k[c] = (act && up) ? mid[c] : lo_k[c];
-            hi_k[c] = (act && !up) ? mid[c] : hi_k[c];
-          }
-        }
-        buf ^= 1;
       }
-      if (!hist || wide_block) break;
-      hist = false;  // narrow brackets (a wide subnet): bisection finish
-      lim = 1;
+      buf ^= 1;
     }
     if (hist) {
       // exact-stake histogram finish (consensus_search), shared by the pair
