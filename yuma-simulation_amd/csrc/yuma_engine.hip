@@ -3186,7 +3186,9 @@ __global__ __launch_bounds__(BS, 1) void k_bonds_elem(BondArgs A) {
 //    correction for their fixed-alpha scenarios (p_corr);
 // History: round 3 K = 2 beat 1 / 3 / 4 / 8 (profiles/r03/ab/
 // c3_scan_group_k.txt); packed-pair f32 math and an XCD-grouped block order
-// lost. Round 4 (rq4, R = 2, liquid split): K = 4 at 3 waves / SIMD (144 /
+// lost. Round 4 also: the dividend partials parked in LDS (32 epochs per
+// block, written by the block after a barrier) took it 6.73-6.78 -> 7.09-7.10 ms
+// (profiles/r04/ab_round8.txt). Round 4 (rq4, R = 2, liquid split): K = 4 at 3 waves / SIMD (144 /
 // 168 VGPRs, 6 VGPRs spilled for Yuma 4) 6.90-6.97 ms against 7.03-7.22 for
 // K = 2 at 4 waves; K = 4 at 2 waves 8.96, K = 4 with R = 1 9.36; the
 // scenario groups of one W slab in consecutive blocks 7.15-7.17
