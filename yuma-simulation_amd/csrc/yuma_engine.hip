@@ -1829,6 +1829,17 @@ __global__ __launch_bounds__(256, 1) void k_rank_s(const float* __restrict__ W,
   }
   float Cc[4];
   load4c<VEC>(C + slice * M, 0, 1, m, M, Cc);
+  // the slice's row sums, their IEEE reciprocals and the stakes staged in LDS
+  // once per block (coalesced), instead of two per-lane scalar loads per row
+  // and a reciprocal per row in every lane
+  __shared__ float rows_d[YUMA_MAX_VALIDATORS], rows_r[YUMA_MAX_VALIDATORS], rows_s[YUMA_MAX_VALIDATORS];
+  for (int j = threadIdx.x; j < V; j += 256) {
+    const float dj = rsd[wsl * V + j];
+    rows_d[j] = dj;
+    rows_r[j] = 1.0f / dj;
+    rows_s[j] = sn[slice * V + j];
+  }
+  __syncthreads();
   float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
   constexpr int B = 8;
   for (int r0 = L.g; r0 < V; r0 += 16 * B) {
@@ -1837,14 +1848,16 @@ __global__ __launch_bounds__(256, 1) void k_rank_s(const float* __restrict__ W,
     for (int i = 0; i < B; ++i) {
       const int rr = min(r0 + 16 * i, V - 1);
       load4c<VEC>(Ws, rr, V, m, M, w[i]);
-      d[i] = rsd[wsl * V + rr];
-      s[i] = sn[slice * V + rr];
+      d[i] = rows_d[rr];
+      s[i] = rows_s[rr];
     }
     if (!YUMA2 || divide) {
       bool slow = false;
 #pragma unroll
       for (int i = 0; i < B; ++i) {
-        const RowDiv rdv = row_div(d[i]);
+        const int rr = min(r0 + 16 * i, V - 1);
+        const float ad = fabsf(d[i]);
+        const RowDiv rdv{d[i], rows_r[rr], ad >= 0x1p-60f && ad <= 0x1p60f};
 #pragma unroll
         for (int c = 0; c < 4; ++c) w[i][c] = div_fast_nz(w[i][c], rdv, slow);
       }
