@@ -1343,7 +1343,8 @@ __global__ __launch_bounds__(256, 3) void k_consensus_p(const float* __restrict_
                                                      int V, int M, long long slice0, int tiles,
                                                      double* __restrict__ craw,
                                                      float* __restrict__ Pout, int wsh,
-                                                     const int* __restrict__ crep) {
+                                                     const int* __restrict__ crep,
+                                                     const float4* __restrict__ rq4) {
   constexpr int R = 16, HR = 8 * R;  // rows per lane, rows per half
   __shared__ __attribute__((aligned(16))) unsigned hb[2 * 32 * kHS];  // per pair: 32 columns
   __shared__ __attribute__((aligned(16))) float rl[4][3 * HR];        // per wave: sums, stakes, 1 / sums
@@ -1364,13 +1365,24 @@ __global__ __launch_bounds__(256, 3) void k_consensus_p(const float* __restrict_
   const float* sn_s = sn + slice * V;
   float* rw = rl[wave];
 
-  // load + normalise (load_norm_w_lds over the half's rows)
-  float dv[2], sv[2];
+  // load + normalise (load_norm_w_lds over the half's rows). With k_rowsum's
+  // screened reciprocals (rq4: {row sum, RN(1 / row sum) or NaN, stake}) a
+  // wave whose rows all passed the screen divides without the per-element
+  // guard; a NaN anywhere sends the wave to IEEE division (the same values)
+  float dv[2], sv[2], rv[2];
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
     const int jj = min(h * HR + lane + 64 * k, V - 1);
-    dv[k] = rsd_s[jj];
-    sv[k] = sn_s[jj];
+    if (rq4 != nullptr) {
+      const float4 q = rq4[slice * V + jj];
+      dv[k] = q.x;
+      rv[k] = q.y;
+      sv[k] = q.z;
+    } else {
+      dv[k] = rsd_s[jj];
+      sv[k] = sn_s[jj];
+      rv[k] = 1.0f / dv[k];
+    }
   }
   float wn[R][4];
   const bool full = r0 + 8 * (R - 1) < V && m + 3 < M;
@@ -1397,12 +1409,45 @@ __global__ __launch_bounds__(256, 3) void k_consensus_p(const float* __restrict_
     dmin = fminf(dmin, fabsf(dv[k]));
     rw[j] = dv[k];
     rw[HR + j] = h * HR + j < V ? sv[k] : 0.0f;
-    rw[2 * HR + j] = 1.0f / dv[k];
+    rw[2 * HR + j] = rv[k];
   }
+  const bool screened = rq4 != nullptr && __all(rv[0] == rv[0] && rv[1] == rv[1]);
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  {
+  if (screened) {
+    typedef float f2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const float d = rw[rg + 8 * i];
+      const float r = rw[2 * HR + rg + 8 * i];
+      const f2 r2 = {r, r}, nd2 = {-d, -d};
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        const f2 a2 = {wn[i][2 * hh], wn[i][2 * hh + 1]};
+        const f2 q = a2 * r2;
+        const f2 e = __builtin_elementwise_fma(nd2, q, a2);
+        const f2 q1 = __builtin_elementwise_fma(e, r2, q);
+        wn[i][2 * hh] = q1[0];
+        wn[i][2 * hh + 1] = q1[1];
+      }
+    }
+    if (!__all(full)) {
+#pragma unroll
+      for (int i = 0; i < R; ++i) mask4(r0 + 8 * i, V, m, M, wn[i]);
+    }
+  } else if (rq4 != nullptr) {  // some row failed the screen: IEEE division
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const float d = rw[rg + 8 * i];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) wn[i][c] = wn[i][c] / d;
+    }
+    if (!__all(full)) {
+#pragma unroll
+      for (int i = 0; i < R; ++i) mask4(r0 + 8 * i, V, m, M, wn[i]);
+    }
+  } else {
     typedef float f2 __attribute__((ext_vector_type(2)));
     unsigned ymin = 0xFFFFFFFFu;
 #pragma unroll
@@ -3867,7 +3912,8 @@ template <bool VEC>
 void launch_consensus(RowCfg rc, long long nblocks, hipStream_t st, const float* W,
                       const float* rsd, const float* sn, const int* sx,
                       const yuma_params_t* prm, int N, int V, int M, long long slice0, int tiles,
-                      double* craw, float* P, int wsh, const int* crep) {
+                      double* craw, float* P, int wsh, const int* crep,
+                      const float4* rq4 = nullptr) {
   switch (rc) {  // wave-owned columns up to 256 validators
     case RC_256_1:
       launch_consensus_w<1, VEC>(nblocks, st, W, rsd, sn, sx, prm, N, V, M, slice0, tiles, craw,
@@ -3889,7 +3935,7 @@ void launch_consensus(RowCfg rc, long long nblocks, hipStream_t st, const float*
       // in the last bit at a tie, inside the tie window the tests allow.
       if (VEC && !wsh && P == nullptr)
         YK_LAUNCH((yk::k_consensus_p<true>), nblocks, 256, st, W, rsd, sn, sx, prm, N, V, M, slice0, tiles,
-                  craw, P, wsh, crep);
+                  craw, P, wsh, crep, rq4);
       else
         launch_consensus_w<16, VEC>(nblocks, st, W, rsd, sn, sx, prm, N, V, M, slice0, tiles, craw, P, wsh,
                                     crep);
@@ -4197,7 +4243,7 @@ int run_impl(int variant, const yuma_params_t* prm, int N, int E, int V, int M, 
       tm.mark(YUMA_PHASE_CONSENSUS);
       if (vec)
         launch_consensus<true>(rc, ns * tiles, st, W, ws.rsd, ws.sn, ws.sx, prm, N, V, M, s0, tiles,
-                               ws.craw, out->P, wsh, crep);
+                               ws.craw, out->P, wsh, crep, ws.rq4);
       else
         launch_consensus<false>(rc, ns * tiles, st, W, ws.rsd, ws.sn, ws.sx, prm, N, V, M, s0,
                                 tiles, ws.craw, out->P, wsh, crep);
