@@ -4109,8 +4109,15 @@ int launch_bonds_elem(hipStream_t st, yk::BondArgs& A) {
       return yk::DP_TV;
     }
   }
-  if (bonds_rows(VEC, hist, A.wsh != 0) != 2)
+  if (bonds_rows(VEC, hist, A.wsh != 0) != 2) {
+    // two rows per lane (one incentive load per two rows, 2 epochs in
+    // flight) once the grid has blocks to spare: c4 1.41 -> 1.38 ms; with
+    // c2's 512 such blocks 0.99 -> 1.31, so one row per lane there
+    const long long blocks_r2 = (long long)A.N * ((A.V + 7) / 8) * ((A.M + 255) / 256);
+    if (blocks_r2 >= 4096)
+      return launch_elem_shape<VARIANT, 2, VEC, 2, VEC, false, 256, 256, yk::DP_QTE>(st, A);
     return launch_elem_shape<VARIANT, 1, VEC, 4, VEC, false, 256, 256, yk::DP_QTE>(st, A);
+  }
   if (hist) return launch_elem_shape<VARIANT, 2, VEC, 2, VEC, true, 256, 64, yk::DP_TV>(st, A);
   return launch_elem_shape<VARIANT, 2, VEC, 2, VEC, false, 256, 64, yk::DP_TV>(st, A);
 }
