@@ -158,3 +158,13 @@ PATCHES["qte_bs128_p6"] = [("    return launch_elem_shape<VARIANT, 1, VEC, 4, VE
                             "    return launch_elem_shape<VARIANT, 1, VEC, 6, VEC, false, 128, 256, yk::DP_QTE>(st, A);")]
 PATCHES["qte_p6"] = [("    return launch_elem_shape<VARIANT, 1, VEC, 4, VEC, false, 256, 256, yk::DP_QTE>(st, A);",
                       "    return launch_elem_shape<VARIANT, 1, VEC, 6, VEC, false, 256, 256, yk::DP_QTE>(st, A);")]
+# streaming rank: rows per batch
+PATCHES["rank_b16"] = [("  float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};\n  constexpr int B = 8;\n  for (int r0 = L.g; r0 < V; r0 += 16 * B) {",
+                        "  float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};\n  constexpr int B = 16;\n  for (int r0 = L.g; r0 < V; r0 += 16 * B) {")]
+PATCHES["rank_b4"] = [("  float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};\n  constexpr int B = 8;\n  for (int r0 = L.g; r0 < V; r0 += 16 * B) {",
+                       "  float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};\n  constexpr int B = 4;\n  for (int r0 = L.g; r0 < V; r0 += 16 * B) {")]
+# history-less scan: two rows per lane (one incentive load per two rows)
+PATCHES["qte_r2p4"] = [("    return launch_elem_shape<VARIANT, 1, VEC, 4, VEC, false, 256, 256, yk::DP_QTE>(st, A);",
+                        "    return launch_elem_shape<VARIANT, 2, VEC, 4, VEC, false, 256, 256, yk::DP_QTE>(st, A);")]
+PATCHES["qte_r2p2"] = [("    return launch_elem_shape<VARIANT, 1, VEC, 4, VEC, false, 256, 256, yk::DP_QTE>(st, A);",
+                        "    return launch_elem_shape<VARIANT, 2, VEC, 2, VEC, false, 256, 256, yk::DP_QTE>(st, A);")]
