@@ -1972,6 +1972,21 @@ __device__ double block_sum_d(double x, double* red) {
   return t;
 }
 
+// h[key] += 1 for every active lane. The lanes holding the first active
+// lane's key add once, by their count: the levels of a slice crowd into a few
+// bins (M = 4096 puts every level of a uniform consensus in high byte 0), and
+// same-address LDS atomics serialise lane by lane. Counts are integers, so the
+// histogram does not depend on how the adds are grouped.
+__device__ inline void hist_add(int* h, int key) {
+  const int k0 = __builtin_amdgcn_readfirstlane(key);
+  const unsigned long long same = __ballot(key == k0);
+  if (key == k0) {
+    if ((int)__lane_id() == __ffsll((long long)same) - 1) atomicAdd(&h[k0], (int)__popcll(same));
+  } else {
+    atomicAdd(&h[key], 1);
+  }
+}
+
 // high-byte histogram of the levels (four loads in flight per thread)
 template <int NT>
 __device__ void hist_high(const int* __restrict__ q, int M, int* hist1) {
@@ -1981,31 +1996,51 @@ __device__ void hist_high(const int* __restrict__ q, int M, int* hist1) {
 #pragma unroll
     for (int u = 0; u < 4; ++u) v[u] = min(max(q[j + u * NT], 0), 65535);
 #pragma unroll
-    for (int u = 0; u < 4; ++u) atomicAdd(&hist1[v[u] >> 8], 1);
+    for (int u = 0; u < 4; ++u) hist_add(hist1, v[u] >> 8);
   }
-  for (; j < M; j += NT) atomicAdd(&hist1[min(max(q[j], 0), 65535) >> 8], 1);
+  for (; j < M; j += NT) hist_add(hist1, min(max(q[j], 0), 65535) >> 8);
 }
 
-// k-th smallest quantisation level (0-based) by a two-level 256-bin integer
-// histogram select. Integer counts are order independent, so the selection is
-// exact and deterministic. hist1 must already hold the high-byte histogram.
-template <int NT>
-__device__ int select_level(const int* __restrict__ q, int M, int k, const int* hist1,
-                            int* hist2, int* bc) {
-  if (threadIdx.x == 0) {
-    int cum = 0, b = 0;
-    for (b = 0; b < 256; ++b) {
-      if (cum + hist1[b] > k) break;
-      cum += hist1[b];
-    }
-    bc[0] = b;
-    bc[1] = k - cum;
+// Bin of the k-th smallest entry of a 256-bin count histogram h: the first bin
+// b with sum(h[0..b]) > k, and k minus the counts below it. One wave (all 64
+// lanes, four bins each, an inclusive shuffle scan) replaces the serial walk
+// of 256 dependent LDS reads; b = 256 when k >= sum(h), as the walk gives.
+__device__ void find_bin(const int* h, int k, int* dst) {
+  const int l = threadIdx.x & 63;
+  const int c0 = h[4 * l], c1 = h[4 * l + 1], c2 = h[4 * l + 2], c3 = h[4 * l + 3];
+  const int s = c0 + c1 + c2 + c3;
+  int incl = s;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(incl, o, 64);
+    if (l >= o) incl += y;
   }
-  for (int j = threadIdx.x; j < 256; j += NT) hist2[j] = 0;
-  __syncthreads();
-  const int b = bc[0];
-  // four levels in flight per thread (a wide subnet has 65536 per slice and
-  // one block per slice: the loop is L2-latency-bound otherwise)
+  const int excl = incl - s;
+  if (excl <= k && k < incl) {
+    int cum = excl, i = 0;
+    if (cum + c0 <= k) {
+      cum += c0;
+      ++i;
+      if (cum + c1 <= k) {
+        cum += c1;
+        ++i;
+        if (cum + c2 <= k) {
+          cum += c2;
+          ++i;
+        }
+      }
+    }
+    dst[0] = 4 * l + i;
+    dst[1] = k - cum;
+  } else if (l == 63 && k >= incl) {
+    dst[0] = 256;
+    dst[1] = k - incl;
+  }
+}
+
+// low-byte histogram of the levels whose high byte is b (four in flight)
+template <int NT>
+__device__ void hist_low(const int* __restrict__ q, int M, int b, int* hist2) {
   int j = threadIdx.x;
   for (; j + 3 * NT < M; j += 4 * NT) {
     int v[4];
@@ -2013,25 +2048,49 @@ __device__ int select_level(const int* __restrict__ q, int M, int k, const int* 
     for (int u = 0; u < 4; ++u) v[u] = min(max(q[j + u * NT], 0), 65535);
 #pragma unroll
     for (int u = 0; u < 4; ++u)
-      if ((v[u] >> 8) == b) atomicAdd(&hist2[v[u] & 255], 1);
+      if ((v[u] >> 8) == b) hist_add(hist2, v[u] & 255);
   }
   for (; j < M; j += NT) {
     const int v = min(max(q[j], 0), 65535);
-    if ((v >> 8) == b) atomicAdd(&hist2[v & 255], 1);
+    if ((v >> 8) == b) hist_add(hist2, v & 255);
+  }
+}
+
+// The k0-th and k1-th smallest quantisation levels (0-based) by a two-level
+// 256-bin integer histogram select. Integer counts are order independent, so
+// the selection is exact and deterministic. hist1 must already hold the
+// high-byte histogram; bc holds 8 ints. The two ranks of one quantile share
+// the low-byte pass when they share a high byte (the usual case).
+template <int NT>
+__device__ int2 select_levels(const int* __restrict__ q, int M, int k0, int k1, const int* hist1,
+                              int* hist2, int* bc) {
+  if (threadIdx.x < 64) {
+    find_bin(hist1, k0, bc);
+    find_bin(hist1, k1, bc + 2);
+  }
+  for (int j = threadIdx.x; j < 256; j += NT) hist2[j] = 0;
+  __syncthreads();
+  const int b0 = bc[0], r0 = bc[1], b1 = bc[2], r1 = bc[3];
+  hist_low<NT>(q, M, b0, hist2);
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    find_bin(hist2, r0, bc + 4);
+    if (b1 == b0) find_bin(hist2, r1, bc + 6);
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    int kk = bc[1], cum = 0, lo = 0;
-    for (lo = 0; lo < 256; ++lo) {
-      if (cum + hist2[lo] > kk) break;
-      cum += hist2[lo];
-    }
-    bc[2] = (b << 8) | lo;
+  int2 lev;
+  lev.x = (b0 << 8) | bc[4];
+  if (b1 != b0) {
+    for (int j = threadIdx.x; j < 256; j += NT) hist2[j] = 0;
+    __syncthreads();
+    hist_low<NT>(q, M, b1, hist2);
+    __syncthreads();
+    if (threadIdx.x < 64) find_bin(hist2, r1, bc + 6);
+    __syncthreads();
   }
+  lev.y = (b1 << 8) | bc[6];
   __syncthreads();
-  const int r = bc[2];
-  __syncthreads();
-  return r;
+  return lev;
 }
 
 
@@ -2044,8 +2103,9 @@ __device__ float quantile_of(const int* q, int M, float qf, const int* hist1, in
   const int lo_i = (int)rank;
   const int hi_i = (int)ceilf(rank);
   const float w = rank - (float)lo_i;
-  const float a = level_value(select_level<NT>(q, M, lo_i, hist1, hist2, bc));
-  const float b = level_value(select_level<NT>(q, M, hi_i, hist1, hist2, bc));
+  const int2 lv = select_levels<NT>(q, M, lo_i, hi_i, hist1, hist2, bc);
+  const float a = level_value(lv.x);
+  const float b = level_value(lv.y);
   const float diff = b - a;
   if (fabsf(w) < 0.5f) return fmaf(w, diff, a);
   return fmaf(-diff, 1.0f - w, b);
@@ -2069,7 +2129,7 @@ __global__ __launch_bounds__(NT) void k_quantise(const double* __restrict__ craw
                                                  int no_liquid, const int* __restrict__ crep) {
   __shared__ float redf[NT / 64];
   __shared__ double redd[NT / 64];
-  __shared__ int hist1[256], hist2[256], bc[4];
+  __shared__ int hist1[256], hist2[256], bc[8];
   const long long slice = slice0 + blockIdx.x;
   const yuma_params_t& p = prm[slice % N];
   const double* cr = craw + rep_slice(crep, slice, N) * M;
@@ -2089,12 +2149,12 @@ __global__ __launch_bounds__(NT) void k_quantise(const double* __restrict__ craw
   } else if (variant == YUMA_VARIANT_RUST) {
     double acc = 0.0;
     int m = threadIdx.x;
-    for (; m + 3 * NT < M; m += 4 * NT) {  // loads in flight, same summation order
-      const double x0 = cr[m], x1 = cr[m + NT], x2 = cr[m + 2 * NT], x3 = cr[m + 3 * NT];
-      acc = acc + x0;
-      acc = acc + x1;
-      acc = acc + x2;
-      acc = acc + x3;
+    for (; m + 7 * NT < M; m += 8 * NT) {  // loads in flight, same summation order
+      double x[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) x[u] = cr[m + u * NT];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc = acc + x[u];
     }
     for (; m < M; m += NT) acc = acc + cr[m];
     sumd = block_sum_d<NT>(acc, redd);
@@ -2102,27 +2162,41 @@ __global__ __launch_bounds__(NT) void k_quantise(const double* __restrict__ craw
   } else {
     float acc = 0.0f;
     int m = threadIdx.x;
-    for (; m + 3 * NT < M; m += 4 * NT) {  // loads in flight, same summation order
-      const double x0 = cr[m], x1 = cr[m + NT], x2 = cr[m + 2 * NT], x3 = cr[m + 3 * NT];
-      acc = acc + (float)x0;
-      acc = acc + (float)x1;
-      acc = acc + (float)x2;
-      acc = acc + (float)x3;
+    for (; m + 7 * NT < M; m += 8 * NT) {  // loads in flight, same summation order
+      double x[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) x[u] = cr[m + u * NT];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc = acc + (float)x[u];
     }
     for (; m < M; m += NT) acc = acc + (float)cr[m];
     sumf = block_sum<NT>(acc, redf);
   }
-  for (int m = threadIdx.x; m < M; m += NT) {
-    int lev;
-    if (variant == YUMA_VARIANT_RUST) {
-      const double x = cr[m] / sumd * 65535.0;
-      lev = (int)x;
-    } else {
-      const float x = (float)cr[m] / sumf * 65535.0f;
-      lev = (int)x;
+  // the levels are kept only for the quantile select here or a shard's
+  // k_liquid later; every other slice needs C alone
+  const bool keep_q = no_liquid || p.liquid_mode == YUMA_LIQUID_QUANTILE;
+  auto level_of = [&](double c) {
+    if (variant == YUMA_VARIANT_RUST) return (int)(c / sumd * 65535.0);
+    return (int)((float)c / sumf * 65535.0f);
+  };
+  {
+    int m = threadIdx.x;
+    for (; m + 7 * NT < M; m += 8 * NT) {  // a wide subnet: 65536 levels per slice
+      double x[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) x[u] = cr[m + u * NT];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int lev = level_of(x[u]);
+        if (keep_q) q[m + u * NT] = lev;
+        Cs[m + u * NT] = level_value(lev);
+      }
     }
-    q[m] = lev;
-    Cs[m] = level_value(lev);
+    for (; m < M; m += NT) {
+      const int lev = level_of(cr[m]);
+      if (keep_q) q[m] = lev;
+      Cs[m] = level_value(lev);
+    }
   }
   float a32 = qnan(), b32 = qnan(), ch = qnan(), cl = qnan();
   // no_liquid: the quantiles need every shard's levels (k_liquid, later stage)
@@ -2277,7 +2351,7 @@ __global__ __launch_bounds__(NT) void k_liquid(const yuma_params_t* __restrict__
                                                float* __restrict__ ba, float* __restrict__ scal,
                                                const float* __restrict__ sumc_f,
                                                const double* __restrict__ sumc_d, int rust) {
-  __shared__ int hist1[256], hist2[256], bc[4];
+  __shared__ int hist1[256], hist2[256], bc[8];
   const long long slice = slice0 + blockIdx.x;
   const yuma_params_t& p = prm[slice % N];
   const int* q = qlev + slice * Mq;
