@@ -168,3 +168,6 @@ PATCHES["qte_r2p4"] = [("    return launch_elem_shape<VARIANT, 1, VEC, 4, VEC, f
                         "    return launch_elem_shape<VARIANT, 2, VEC, 4, VEC, false, 256, 256, yk::DP_QTE>(st, A);")]
 PATCHES["qte_r2p2"] = [("    return launch_elem_shape<VARIANT, 1, VEC, 4, VEC, false, 256, 256, yk::DP_QTE>(st, A);",
                         "    return launch_elem_shape<VARIANT, 2, VEC, 2, VEC, false, 256, 256, yk::DP_QTE>(st, A);")]
+# finalize: all four quads of a thread's group in flight (c3: 16 quads per slice)
+PATCHES["fin_u4"] = [("#pragma unroll 2\n      for (int b = tg; b < nq; b += 4) {\n        float4 x[4];",
+                      "#pragma unroll 4\n      for (int b = tg; b < nq; b += 4) {\n        float4 x[4];")]

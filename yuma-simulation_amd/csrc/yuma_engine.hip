@@ -2443,6 +2443,24 @@ __global__ __launch_bounds__(256) void k_incentive(float* __restrict__ Rio,
   __syncthreads();
   const float sr = tot;
   const int m1 = min(M, (ch + 1) * kIncCols);
+  if ((M & 3) == 0) {  // 16-byte rows: one float4 per lane (c3 writes R and I of 16384 slices)
+    const float4* r4 = reinterpret_cast<const float4*>(Rio + rs * M);
+    float4* d4 = reinterpret_cast<float4*>(Rio + slice * M);
+    float4* i4 = reinterpret_cast<float4*>(I + slice * M);
+    for (int j = ch * (kIncCols / 4) + threadIdx.x; j < m1 / 4; j += 256) {
+      const float4 r = r4[j];
+      if (rs != slice) d4[j] = r;
+      i4[j] = make_float4(nan_to_num(r.x / sr, 0.0f), nan_to_num(r.y / sr, 0.0f),
+                          nan_to_num(r.z / sr, 0.0f), nan_to_num(r.w / sr, 0.0f));
+      if (T != nullptr) {
+        const float4 pv = reinterpret_cast<const float4*>(Pin + slice * M)[j];
+        reinterpret_cast<float4*>(T + slice * M)[j] =
+            make_float4(nan_to_num(r.x / pv.x, 0.0f), nan_to_num(r.y / pv.y, 0.0f),
+                        nan_to_num(r.z / pv.z, 0.0f), nan_to_num(r.w / pv.w, 0.0f));
+      }
+    }
+    return;
+  }
   for (int m = ch * kIncCols + threadIdx.x; m < m1; m += 256) {
     const float r = Rio[rs * M + m];
     if (rs != slice) Rio[slice * M + m] = r;
