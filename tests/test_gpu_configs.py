@@ -272,6 +272,9 @@ def test_wide_float_weights_against_oracle():
     (engine.VARIANT_YUMA4, {}, None, 0, ("R", "D"), 7),
     (engine.VARIANT_YUMA4, {}, (4, 7, "zero"), 0, ("R", "D"), 7),
     (engine.VARIANT_YUMA4, {"liquid_alpha": True}, (2, 7, "zero"), 3, (), 5),
+    # liquid alpha on odd scenarios only: classes whose representative is not
+    # liquid still select quantiles once for their liquid members
+    (engine.VARIANT_YUMA4, {"liquid_odd": True}, None, 0, ("R", "D"), 6),
     # the column-normalised strip scan (k_bonds_cn: V > 64), padded rows
     (engine.VARIANT_RUST, {"liquid_alpha": True}, None, 4, ("R", "D"), (5, 200)),
     (engine.VARIANT_YUMA1, {}, None, 0, ("R", "D", "T", "Tv"), (6, 130)),
@@ -300,7 +303,9 @@ def test_shared_input_sweep_equals_replicated(variant, extra, reset, chunk, want
     cfgs = []
     for i in range(N):
         sim = {k: v for k, v in extra.items() if k in ("bond_penalty",)}
-        prm = {k: v for k, v in extra.items() if k not in ("bond_penalty",)}
+        prm = {k: v for k, v in extra.items() if k not in ("bond_penalty", "liquid_odd")}
+        if extra.get("liquid_odd"):
+            prm["liquid_alpha"] = i % 2 == 1
         cfgs.append(YumaConfig(simulation=bench_sim(kappa=0.3 + 0.08 * (i % 3), **sim),
                                yuma_params=YumaParams(bond_alpha=0.05 + 0.05 * i, **prm)))
     kw = {}
