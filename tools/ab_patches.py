@@ -171,3 +171,8 @@ PATCHES["qte_r2p2"] = [("    return launch_elem_shape<VARIANT, 1, VEC, 4, VEC, f
 # finalize: all four quads of a thread's group in flight (c3: 16 quads per slice)
 PATCHES["fin_u4"] = [("#pragma unroll 2\n      for (int b = tg; b < nq; b += 4) {\n        float4 x[4];",
                       "#pragma unroll 4\n      for (int b = tg; b < nq; b += 4) {\n        float4 x[4];")]
+# history-less scan on large grids: 16 / 32 rows per block (fewer incentive re-reads per epoch)
+PATCHES["qte_r2p2_bs512"] = [("      return launch_elem_shape<VARIANT, 2, VEC, 2, VEC, false, 256, 256, yk::DP_QTE>(st, A);",
+                              "      return launch_elem_shape<VARIANT, 2, VEC, 2, VEC, false, 512, 256, yk::DP_QTE>(st, A);")]
+PATCHES["qte_r2p2_bs1024"] = [("      return launch_elem_shape<VARIANT, 2, VEC, 2, VEC, false, 256, 256, yk::DP_QTE>(st, A);",
+                               "      return launch_elem_shape<VARIANT, 2, VEC, 2, VEC, false, 1024, 256, yk::DP_QTE>(st, A);")]
