@@ -176,3 +176,6 @@ PATCHES["qte_r2p2_bs512"] = [("      return launch_elem_shape<VARIANT, 2, VEC, 2
                               "      return launch_elem_shape<VARIANT, 2, VEC, 2, VEC, false, 512, 256, yk::DP_QTE>(st, A);")]
 PATCHES["qte_r2p2_bs1024"] = [("      return launch_elem_shape<VARIANT, 2, VEC, 2, VEC, false, 256, 256, yk::DP_QTE>(st, A);",
                                "      return launch_elem_shape<VARIANT, 2, VEC, 2, VEC, false, 1024, 256, yk::DP_QTE>(st, A);")]
+# paired consensus at 2 / 5 waves per SIMD
+PATCHES["cp_lb2"] = [("__global__ __launch_bounds__(256, 3) void k_consensus_p(", "__global__ __launch_bounds__(256, 2) void k_consensus_p(")]
+PATCHES["cp_lb5"] = [("__global__ __launch_bounds__(256, 3) void k_consensus_p(", "__global__ __launch_bounds__(256, 5) void k_consensus_p(")]
