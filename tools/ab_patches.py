@@ -179,3 +179,6 @@ PATCHES["qte_r2p2_bs1024"] = [("      return launch_elem_shape<VARIANT, 2, VEC, 
 # paired consensus at 2 / 5 waves per SIMD
 PATCHES["cp_lb2"] = [("__global__ __launch_bounds__(256, 3) void k_consensus_p(", "__global__ __launch_bounds__(256, 2) void k_consensus_p(")]
 PATCHES["cp_lb5"] = [("__global__ __launch_bounds__(256, 3) void k_consensus_p(", "__global__ __launch_bounds__(256, 5) void k_consensus_p(")]
+# finalize: one quad of a thread's group in flight
+PATCHES["fin_u1"] = [("#pragma unroll 2\n      for (int b = tg; b < nq; b += 4) {\n        float4 x[4];",
+                      "#pragma unroll 1\n      for (int b = tg; b < nq; b += 4) {\n        float4 x[4];")]
