@@ -66,10 +66,10 @@ def phase_bytes(phase: str, V: int, M: int, variant: int, liquid: bool, hist: bo
     and the per-epoch row sums are read once per input epoch for all of them,
     so their bytes are divided among the wshare scenarios."""
     tiles = (M + 63) // 64
-    # dividend partials per (slice, validator): 16-miner strips (column-
-    # normalised strip scan), quads of 64-miner tiles (the wide history scan
-    # and the history-less one-row scan), else one per tile (the sweep scan)
-    if variant <= 2:
+    # dividend partials per (slice, validator): 16-miner strips (YumaRust's
+    # column-normalised strip scan), quads of 64-miner tiles (the wide history
+    # scan and the history-less one-row scan), else one per tile (the sweep scan)
+    if variant == 0:
         ptiles = (M + 15) // 16
     elif wshare == 1 and (not hist or M >= 1024):
         ptiles = (tiles + 3) // 4
@@ -81,10 +81,13 @@ def phase_bytes(phase: str, V: int, M: int, variant: int, liquid: bool, hist: bo
     table = {
         "consensus": w + 8 * V + 8 * M,
         "quantise": 8 * M + 8 * M + (4 * M if liquid else 0),
-        "rank": w + 8 * V + 4 * M + 4 * M + 4 * tiles,
+        # Yuma / Yuma2 also write the bond column sums csb [M]
+        "rank": w + 8 * V + 4 * M + 4 * M + 4 * tiles + (4 * M if variant in (1, 2) else 0),
         "rowsum": w + (4 * V + 8 * V + 16 * V) / wshare,
         "incentive": 4 * M + 4 * tiles + 4 * M,
-        "bonds": (w + 8 * V + 4 * M + (4 * M if colnorm else 0) + (4 * M if liquid else 0)
+        # column-normalised variants read C and a column sum per miner (Yuma /
+        # Yuma2: csb; YumaRust: its rank R)
+        "bonds": (w + 8 * V + 4 * M + (8 * M if colnorm else 0) + (4 * M if liquid else 0)
                   + (4 * VM if hist else 0) + 4 * V * ptiles + 8 * VM / max(chunk, 1)),
         "finalize": 4 * V * ptiles + 4 * V + 4 * V,
     }
@@ -99,11 +102,14 @@ def kernel_of(phase: str, variant: int, shared: bool = False, V: int = 256, M: i
               N: int = 1) -> str:
     """The kernel that runs a phase (as rocprofv3 names it) for run outputs:
     the bond scan is k_bonds_elem for Yuma 3/4 (k_bonds_grp for a sweep over
-    one shared input trajectory), and for YumaRust / Yuma 1 / Yuma 2 the strip
-    scan k_bonds_cn above 64 validators (k_bonds on 64-miner tiles below)."""
+    one shared input trajectory) and, above 64 validators, for Yuma 1 / 2
+    (the rank pass forms their bond column sums); YumaRust's strip scan
+    k_bonds_cn above 64 validators; k_bonds on 64-miner tiles below."""
     if phase == "bonds":
         if variant >= 3:
             return "k_bonds_grp" if shared and N > 1 else "k_bonds_elem"
+        if variant in (1, 2) and V > 64:
+            return "k_bonds_elem"
         return "k_bonds_cn" if V > 64 and M % 4 == 0 else "k_bonds"
     if phase == "consensus" and 64 < V <= 256 and M % 4 == 0 and not shared:
         return "k_consensus_p"  # 128-byte row segments (wave pairs; run outputs)

@@ -72,9 +72,10 @@ def _shared_vs_replicated_and_oracle(ids: list[int], E: int, oracle_ids: list[in
     """The launch `bench.py --config c3` times: every scenario reads ONE W/S
     trajectory (shared_inputs, yuma_run_ex YUMA_RUN_SHARED_INPUTS), no bond
     history. At 256 x 4096 that is the shared-input bond scan
-    (launch_bonds_elem: k_bonds_grp<YUMA4, K=2, R=1, P=2>, two scenarios per
-    block over one W tile), the row sums once per input epoch and the consensus / quantisation input /
-    rank once per consensus class (k_classes). C, Dn, I and B_final must be
+    (launch_bonds_elem: k_bonds_grp<YUMA4, K=4, R=2, P=2>, four scenarios per
+    block over one 32-row x 64-miner W tile), the row sums once per input
+    epoch and the consensus / quantisation input / rank once per consensus
+    class (k_classes). C, Dn, I and B_final must be
     bitwise those of the same run on W and S replicated per scenario (every
     scenario computing its own everything), and each scenario in oracle_ids
     must match the oracle's run_simulation loop (C exact, the rest 1e-5)."""
@@ -230,6 +231,47 @@ def test_random_float_epochs_tie_window(variant, version, record_property):
     assert_close(res.Dn[:, 0].cpu().numpy(), ref["Dn"], what="Dn")
     assert_close(res.I[:, 0].cpu().numpy(), ref["I"], what="I")
     assert_close(res.B_hist[:, 0].cpu().numpy(), ref["B"], what="B")
+
+
+@pytest.mark.parametrize("V,M", [(256, 4096), (200, 1000)])
+def test_paired_and_wave_consensus_agree_on_float_stakes(V, M, record_property):
+    """runs without the prerank P take the paired consensus kernel
+    (k_consensus_p: each wave pair's stake sums go h0 + h1), runs with P the
+    wave-owned one (k_consensus_w, another addition order). On generic float
+    stakes (no exact-stake histogram finish: both bisect) their C may differ
+    only in columns inside the oracle's tie window; at this seed none flips,
+    so C is bitwise equal. Against the oracle (numpy's summation order) C is
+    equal outside the tie window, and Dn within 1e-5 on every epoch whose
+    columns all agree (yumas.py:195-211)."""
+    E = 6
+    rng = np.random.default_rng(0xC0 + V)
+    W = rng.random((E, 1, V, M), dtype=np.float32)
+    W *= rng.random((E, 1, V, M), dtype=np.float32) < 0.6
+    S = rng.random((E, 1, V), dtype=np.float32) + np.float32(1e-3)
+    cfg = YumaConfig()
+    params = [engine.make_params(engine.VARIANT_YUMA3, cfg)]
+    a = engine.run(engine.VARIANT_YUMA3, params, torch.from_numpy(W), torch.from_numpy(S))
+    b = engine.run(engine.VARIANT_YUMA3, params, torch.from_numpy(W), torch.from_numpy(S), want=("P",))
+    torch.cuda.synchronize()
+    Ca, Cb = a.C[:, 0].cpu().numpy(), b.C[:, 0].cpu().numpy()
+    ref = orc.run("Yuma 3 (Rhef)", W[:, 0], S[:, 0], cfg)
+    win = flips = checked = 0
+    Dn = a.Dn[:, 0].cpu().numpy()
+    for e in range(E):
+        flags = orc.tie_columns(W[e, 0], S[e, 0], cfg.kappa, cfg.consensus_precision)
+        win += int(flags.sum())
+        assert not ((Ca[e] != Cb[e]) & ~flags).any(), f"epoch {e}: kernels differ outside the tie window"
+        out, _, inside = _tie_report(Ca[e], ref["C"][e], W[e, 0], S[e, 0], cfg)
+        assert out == 0, f"epoch {e}: {out} columns differ from the oracle outside the tie window"
+        flips += inside
+        if flips == 0:  # no flipped column so far, none carried by the bond state
+            assert_close(Dn[e], ref["Dn"][e], what=f"Dn[{e}]")
+            checked += 1
+    record_property("tie_window_columns", win)
+    record_property("tie_window_flips_vs_oracle", flips)
+    print(f"\n{V}x{M}: tie window {win} columns, {flips} flipped against the oracle, Dn checked on {checked} epochs")
+    np.testing.assert_array_equal(Ca, Cb)
+    assert checked >= 1
 
 
 def test_wide_float_weights_against_oracle():

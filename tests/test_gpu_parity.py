@@ -362,11 +362,13 @@ def test_multi_epoch_vs_oracle_and_chunk_invariance(variant):
 
 
 @pytest.mark.parametrize("V,vids", [(64, (engine.VARIANT_YUMA1, engine.VARIANT_YUMA4)),
-                                     (160, (engine.VARIANT_RUST, engine.VARIANT_YUMA1, engine.VARIANT_YUMA2))])
+                                     (160, (engine.VARIANT_RUST, engine.VARIANT_YUMA1, engine.VARIANT_YUMA2)),
+                                     (384, (engine.VARIANT_RUST, engine.VARIANT_YUMA1, engine.VARIANT_YUMA2))])
 def test_batched_scenarios_equal_individual_runs(V, vids):
     """N scenarios in one launch == each alone (bitwise), params differing.
-    V = 160: the column-normalised strip scan (k_bonds_cn) with padded rows
-    and a half-filled last 16-miner strip."""
+    V = 160: the column-normalised bond scans with padded rows and a
+    half-filled last 16-miner strip; V = 384: 257-512 validators
+    on the float4 path (YumaRust's strip scan with four rows per lane)."""
     E, N, M = 6, 5, 1000  # M % 4 == 0 but not a multiple of 64 (nor of 16)
     W = synth.weights(77, E, N, V, M)
     S = synth.stakes(77, E, N, V, period=3)

@@ -291,7 +291,9 @@ def test_bench_line_helpers():
             assert bench.kernel_of(phase, variant).startswith("k_")
     assert bench.kernel_of("bonds", engine.VARIANT_YUMA3) == "k_bonds_elem"
     assert bench.kernel_of("bonds", engine.VARIANT_YUMA4, shared=True, N=512) == "k_bonds_grp"
-    assert bench.kernel_of("bonds", engine.VARIANT_YUMA1) == "k_bonds_cn"
+    assert bench.kernel_of("bonds", engine.VARIANT_YUMA1) == "k_bonds_elem"  # rank-formed column sums
+    assert bench.kernel_of("bonds", engine.VARIANT_YUMA2) == "k_bonds_elem"
+    assert bench.kernel_of("bonds", engine.VARIANT_RUST) == "k_bonds_cn"
     assert bench.kernel_of("bonds", engine.VARIANT_YUMA1, V=64) == "k_bonds"  # below 65 validators
     assert bench.kernel_of("rank", engine.VARIANT_YUMA2) == "k_rank_s"
     assert bench.kernel_of("consensus", engine.VARIANT_YUMA3) == "k_consensus_p"

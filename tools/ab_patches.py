@@ -182,3 +182,49 @@ PATCHES["cp_lb5"] = [("__global__ __launch_bounds__(256, 3) void k_consensus_p("
 # finalize: one quad of a thread's group in flight
 PATCHES["fin_u1"] = [("#pragma unroll 2\n      for (int b = tg; b < nq; b += 4) {\n        float4 x[4];",
                       "#pragma unroll 1\n      for (int b = tg; b < nq; b += 4) {\n        float4 x[4];")]
+
+# round 5: k_consensus_p with one wave pair per block (a 2-wave block per
+# 32-miner group: the block barriers wait for the partner wave only)
+PATCHES["cons_np1"] = [("constexpr int kConsPairs = 2;", "constexpr int kConsPairs = 1;")]
+
+# round 5: Yuma / Yuma2 on the wide element-wise history scan (k_bonds_elem
+# with the rank pass's column sums): ring depth, clip form, division form
+PATCHES["cn_p3"] = [("constexpr int kWidePCn = 2;", "constexpr int kWidePCn = 3;")]
+PATCHES["cn_p4"] = [("constexpr int kWidePCn = 2;", "constexpr int kWidePCn = 4;")]
+PATCHES["cn_vmin"] = [("            const float wc = tmin(src, rcc[k][c]);\n            const float wb = p_ompen",
+                       "            const float wc = vmin(src, rcc[k][c]);\n            const float wb = p_ompen")]
+PATCHES["cn_rcp"] = [(
+    """#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            const float src = (YUMA2 && have_wp) ? Wp[i][c] : wn[c];
+            const float wc = tmin(src, rcc[k][c]);
+            const float wb = p_ompen * src + p_pen * wc;
+            const float b = nan_to_num((rsn[k][i] * wb) / rcs[k][c], 0.0f);
+            B[i][c] = has_old ? bac[c] * b + omba[c] * B[i][c] : b;
+            if (YUMA2) Wp[i][c] = wn[c];
+          }""",
+    """          RowDiv csd[4];
+#pragma unroll
+          for (int c = 0; c < 4; ++c) csd[c] = row_div(rcs[k][c]);
+          float num[4], bq[4];
+          bool slow2 = false;
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            const float src = (YUMA2 && have_wp) ? Wp[i][c] : wn[c];
+            const float wc = tmin(src, rcc[k][c]);
+            const float wb = p_ompen * src + p_pen * wc;
+            num[c] = rsn[k][i] * wb;
+            bq[c] = div_fast(num[c], csd[c], slow2);
+          }
+          if (__any(slow2)) {
+#pragma unroll
+            for (int c = 0; c < 4; ++c) bq[c] = num[c] / rcs[k][c];
+          }
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            const float b = nan_to_num(bq[c], 0.0f);
+            B[i][c] = has_old ? bac[c] * b + omba[c] * B[i][c] : b;
+            if (YUMA2) Wp[i][c] = (YUMA2 && have_wp) ? wn[c] : wn[c];
+          }""")]
+PATCHES["cn_rcp_p3"] = PATCHES["cn_rcp"] + PATCHES["cn_p3"]
+PATCHES["cn_vmin_p3"] = PATCHES["cn_vmin"] + PATCHES["cn_p3"]

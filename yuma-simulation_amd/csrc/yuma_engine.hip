@@ -153,8 +153,10 @@ __device__ __forceinline__ long long in_slice(long long slice, int N, int wsh) {
 // take its results (bitwise the same computation). Every other parameter
 // (bond α, liquid α, resets, ...) stays per scenario.
 constexpr int kClassKeys = 4096;  // scenarios whose class keys fit in LDS (64 KiB)
+// with_penalty: the key also holds bond_penalty (Yuma's rank pass forms the
+// bond column sums Σ_v S·W_b, which depend on it)
 __global__ __launch_bounds__(256) void k_classes(const yuma_params_t* __restrict__ prm, int N,
-                                                 int* __restrict__ crep) {
+                                                 int* __restrict__ crep, int with_penalty) {
   if (N <= kClassKeys) {
     // the keys staged once per block: the first-match walk then reads LDS,
     // not one dependent 3-field global load per scenario (c3: 69 us per run)
@@ -162,7 +164,7 @@ __global__ __launch_bounds__(256) void k_classes(const yuma_params_t* __restrict
     for (int j = threadIdx.x; j < N; j += 256) {
       const yuma_params_t& b = prm[j];
       key[j] = make_uint4(__float_as_uint(b.kappa), (unsigned)b.bisect_iters,
-                          b.flags & YUMA_FLAG_NO_HIST, 0u);
+                          b.flags & YUMA_FLAG_NO_HIST, with_penalty ? __float_as_uint(b.bond_penalty) : 0u);
     }
     __syncthreads();
     for (int n = blockIdx.x * 256 + threadIdx.x; n < N; n += gridDim.x * 256) {
@@ -170,7 +172,7 @@ __global__ __launch_bounds__(256) void k_classes(const yuma_params_t* __restrict
       int r = n;
       for (int j = 0; j < n; ++j) {
         const uint4 b = key[j];
-        if (b.x == a.x && b.y == a.y && b.z == a.z) {
+        if (b.x == a.x && b.y == a.y && b.z == a.z && b.w == a.w) {
           r = j;
           break;
         }
@@ -186,7 +188,8 @@ __global__ __launch_bounds__(256) void k_classes(const yuma_params_t* __restrict
     for (int j = 0; j < n; ++j) {
       const yuma_params_t& b = prm[j];
       if (__float_as_uint(b.kappa) == ka && b.bisect_iters == a.bisect_iters &&
-          (b.flags & YUMA_FLAG_NO_HIST) == ha) {
+          (b.flags & YUMA_FLAG_NO_HIST) == ha &&
+          (!with_penalty || __float_as_uint(b.bond_penalty) == __float_as_uint(a.bond_penalty))) {
         r = j;
         break;
       }
@@ -1359,8 +1362,11 @@ __device__ __forceinline__ int iscan8_excl(int x, int r8) {
   return y - x;
 }
 
-template <bool VEC>
-__global__ __launch_bounds__(256, 3) void k_consensus_p(const float* __restrict__ W,
+// NP: wave pairs per block (2: a 64-miner tile per 4-wave block; 1: a
+// 32-miner group per 2-wave block, so a block barrier waits for the pair only)
+constexpr int kConsPairs = 2;
+template <bool VEC, int NP = 2>
+__global__ __launch_bounds__(128 * NP, 3) void k_consensus_p(const float* __restrict__ W,
                                                      const float* __restrict__ rsd,
                                                      const float* __restrict__ sn,
                                                      const int* __restrict__ sx,
@@ -1371,19 +1377,21 @@ __global__ __launch_bounds__(256, 3) void k_consensus_p(const float* __restrict_
                                                      const int* __restrict__ crep,
                                                      const float4* __restrict__ rq4) {
   constexpr int R = 16, HR = 8 * R;  // rows per lane, rows per half
-  __shared__ __attribute__((aligned(16))) unsigned hb[2 * 32 * kHS];  // per pair: 32 columns
-  __shared__ __attribute__((aligned(16))) float rl[4][3 * HR];        // per wave: sums, stakes, 1 / sums
-  __shared__ float xf[2][4][32];  // float exchange, double-buffered
-  __shared__ int xi[2][4][32];    // bracket max / min bit patterns
-  __shared__ unsigned xflag[2][4];
+  constexpr int NWV = 2 * NP;         // waves per block
+  __shared__ __attribute__((aligned(16))) unsigned hb[NP * 32 * kHS];  // per pair: 32 columns
+  __shared__ __attribute__((aligned(16))) float rl[NWV][3 * HR];        // per wave: sums, stakes, 1 / sums
+  __shared__ float xf[2][NWV][32];  // float exchange, double-buffered
+  __shared__ int xi[2][NWV][32];    // bracket max / min bit patterns
+  __shared__ unsigned xflag[2][NWV];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int pair = wave >> 1, h = wave & 1, pw = wave ^ 1;
   const int cq = lane >> 3, rg = lane & 7;
-  const long long slice = slice0 + blockIdx.x / tiles;
-  const int tile = blockIdx.x % tiles;
+  const int ctiles = NP == 2 ? tiles : (M + 31) / 32;  // column groups of 32 NP miners per slice
+  const long long slice = slice0 + blockIdx.x / ctiles;
+  const int tile = blockIdx.x % ctiles;
   const int n = (int)(slice % N);
   if (dup_slice(crep, slice, N)) return;  // block-uniform
-  const int m = tile * kTileM + pair * 32 + cq * 4;
+  const int m = tile * (32 * NP) + pair * 32 + cq * 4;
   const int r0 = h * HR + rg;  // this lane's rows r0 + 8 i
   const float* Ws = W + in_slice(slice, N, wsh) * (long long)V * M;
   const float* rsd_s = rsd + slice * V;
@@ -1631,7 +1639,7 @@ __global__ __launch_bounds__(256, 3) void k_consensus_p(const float* __restrict_
     // search needs no activity flags and no closing all-idle pass
     int wmax;
     {
-      const int pl = lane >> 5, cl = lane & 31;
+      const int pl = NP == 2 ? lane >> 5 : 0, cl = lane & 31;
       int lo, hi;
       bracket_of(max(xi[0][2 * pl][cl], xi[0][2 * pl + 1][cl]), min(xi[1][2 * pl][cl], xi[1][2 * pl + 1][cl]),
                  xf[0][2 * pl][0] + xf[0][2 * pl + 1][0], lo, hi);
@@ -1867,7 +1875,13 @@ __global__ __launch_bounds__(256) void k_rank_w(
 // instead (yumas.py:299-300, 328-331: W_prev, at the first epoch the caller's
 // W_prev or W itself) with this epoch's stakes: the previous slice divided by
 // its own row sums — only W_prev is read, not W.
-template <bool VEC, bool YUMA2 = false>
+// BCS (Yuma / Yuma2): the same pass also forms the column sums of the
+// instantaneous bond numerator, csb[m] = Σ_v S·W_b with W_b = (1-β)·src +
+// β·min(src, C) (yumas.py:227-228, :341-342; src = W, Yuma2's W_prev). They
+// depend on the epoch's inputs only, so the bond scan then runs element-wise
+// (k_bonds_elem) instead of reducing every column over all validators each
+// epoch. Same summation order as R.
+template <bool VEC, bool YUMA2 = false, bool BCS = false>
 __global__ __launch_bounds__(256, 1) void k_rank_s(const float* __restrict__ W,
                                                 const float* __restrict__ rsd,
                                                 const float* __restrict__ sn,
@@ -1876,12 +1890,21 @@ __global__ __launch_bounds__(256, 1) void k_rank_s(const float* __restrict__ W,
                                                 float* __restrict__ Rout,
                                                 float* __restrict__ rpart, int wsh,
                                                 const int* __restrict__ crep,
-                                                const float* __restrict__ Wprev_init) {
+                                                const float* __restrict__ Wprev_init,
+                                                float* __restrict__ csb,
+                                                const yuma_params_t* __restrict__ prm) {
   __shared__ float4 red[4][16];
+  __shared__ float4 red2[BCS ? 4 : 1][16];
   const Lay L = lay();
   const long long slice = slice0 + blockIdx.x / tiles;
   const int tile = blockIdx.x % tiles;
   if (dup_slice(crep, slice, N)) return;  // block-uniform
+  float p_pen = 0.0f, p_ompen = 0.0f;
+  if (BCS) {
+    const yuma_params_t& pg = prm[slice % N];
+    p_pen = pg.bond_penalty;
+    p_ompen = pg.one_minus_bond_penalty;
+  }
   const long long VM = (long long)V * M;
   const int m = tile * kTileM + L.c4 * 4;
   // the clipped matrix and the row sums that normalise it (block-uniform)
@@ -1911,6 +1934,7 @@ __global__ __launch_bounds__(256, 1) void k_rank_s(const float* __restrict__ W,
   }
   __syncthreads();
   float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  float acb[4] = {0.0f, 0.0f, 0.0f, 0.0f};
   constexpr int B = 8;
   for (int r0 = L.g; r0 < V; r0 += 16 * B) {
     float w[B][4], d[B], s[B];
@@ -1947,14 +1971,24 @@ __global__ __launch_bounds__(256, 1) void k_rank_s(const float* __restrict__ W,
       const bool live = r0 + 16 * i < V;
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
-        const float x = s[i] * vmin(w[i][c], Cc[c]);
+        const float wc = vmin(w[i][c], Cc[c]);
+        const float x = s[i] * wc;
         acc[c] = live ? acc[c] + x : acc[c];
+        if (BCS) {
+          const float y = s[i] * (p_ompen * w[i][c] + p_pen * wc);
+          acb[c] = live ? acb[c] + y : acb[c];
+        }
       }
     }
   }
 #pragma unroll
   for (int c = 0; c < 4; ++c) acc[c] = sum_rowgroups(acc[c]);
   if (L.lane < 16) red[L.wave][L.c4] = make_float4(acc[0], acc[1], acc[2], acc[3]);
+  if (BCS) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acb[c] = sum_rowgroups(acb[c]);
+    if (L.lane < 16) red2[L.wave][L.c4] = make_float4(acb[0], acb[1], acb[2], acb[3]);
+  }
   __syncthreads();
   if (L.wave == 0) {
     // lane l: miner tile*64 + l
@@ -1967,6 +2001,13 @@ __global__ __launch_bounds__(256, 1) void k_rank_s(const float* __restrict__ W,
     float t = mg < M ? r : 0.0f;
     t = wave_sum(t);
     if (L.lane == 0) rpart[slice * tiles + tile] = t;
+  } else if (BCS && L.wave == 1) {
+    const float* rf = reinterpret_cast<const float*>(&red2[0][0]);
+    float r = rf[L.lane];
+#pragma unroll
+    for (int w = 1; w < 4; ++w) r = r + rf[w * 64 + L.lane];
+    const int mg = tile * kTileM + L.lane;
+    if (mg < M) csb[slice * M + mg] = r;
   }
 }
 
@@ -2436,7 +2477,7 @@ __global__ __launch_bounds__(256) void k_incentive(float* __restrict__ Rio,
                                                    float* __restrict__ scal,
                                                    const float* __restrict__ ext_rsum,
                                                    const int* __restrict__ crep, int N,
-                                                   int nchunk) {
+                                                   int nchunk, int v4) {
   // block = (slice, chunk of kIncCols miners): every block of a slice forms
   // the same ΣR (same order, same bits), then scales its own chunk
   constexpr int kStage = 4096;
@@ -2468,7 +2509,7 @@ __global__ __launch_bounds__(256) void k_incentive(float* __restrict__ Rio,
   __syncthreads();
   const float sr = tot;
   const int m1 = min(M, (ch + 1) * kIncCols);
-  if ((M & 3) == 0) {  // 16-byte rows: one float4 per lane (c3 writes R and I of 16384 slices)
+  if (v4) {  // M % 4 == 0, 16-byte aligned rows: one float4 per lane (c3 writes R and I of 16384 slices)
     const float4* r4 = reinterpret_cast<const float4*>(Rio + rs * M);
     float4* d4 = reinterpret_cast<float4*>(Rio + slice * M);
     float4* i4 = reinterpret_cast<float4*>(I + slice * M);
@@ -2519,6 +2560,8 @@ struct BondArgs {
   float* Binst_out;
   float* dpart;
   const float4* rq4;  // per input slice and row {row sum, RN(1 / row sum) or NaN, stake, 0} (k_rowsum)
+  const float* csb;   // Yuma / Yuma2: [slice][M] Σ_v S·W_b (k_rank_s), or null
+  const float* R;     // [slice][M] rank R = Σ_v S·Wc (YumaRust's first bond column sum)
   int N, V, M, tiles, rowblocks, t0, t1;
   int wsh;      // every scenario reads input slice t (yuma_run_shared)
   int cblocks;  // k_bonds_elem: column blocks of CB miners per row block
@@ -2947,8 +2990,10 @@ __global__ __launch_bounds__(512, 1) void k_bonds_cn(BondArgs A) {
   }
 
   // the inputs of the next P epochs in flight: W rows, row sums, stakes, and
-  // the strip's consensus, incentive and (liquid) bond_alpha
-  float rw[P][R][4], rd[P][R], rsn[P][R], rcc[P][4], ri[P][4], rba[P][4];
+  // the strip's consensus, incentive and (liquid) bond_alpha; YumaRust also
+  // its rank R, which is its first bond column sum: B_sum = Σ_v S·Wc
+  // (yumas.py:113-114) is R's expression (:103), formed once by the rank pass
+  float rw[P][R][4], rd[P][R], rsn[P][R], rcc[P][4], ri[P][4], rba[P][4], rrk[P][4];
   auto fetch = [&](int k, int t) {
     const long long slice = (long long)t * N + n;
     const float* Wt = A.W + (A.wsh ? (long long)t : slice) * VM;
@@ -2966,6 +3011,7 @@ __global__ __launch_bounds__(512, 1) void k_bonds_cn(BondArgs A) {
     load4c<true>(A.C + slice * M, 0, 1, m, M, rcc[k]);
     load4c<true>(A.I + slice * M, 0, 1, m, M, ri[k]);
     if (liquid) load4c<true>(A.ba + slice * M, 0, 1, m, M, rba[k]);
+    if (RUST) load4c<true>(A.R + slice * M, 0, 1, m, M, rrk[k]);
   };
 #pragma unroll
   for (int k = 0; k < P; ++k)
@@ -3031,9 +3077,15 @@ __global__ __launch_bounds__(512, 1) void k_bonds_cn(BondArgs A) {
       float ic[4];
 #pragma unroll
       for (int c = 0; c < 4; ++c) ic[c] = ri[k][c];
+      if constexpr (RUST) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) csum[c] = rrk[k][c];
+      }
       if (t + P < A.t1) fetch(k, t + P);  // slot k consumed: refill it
-      cn_wave_sums(csum, red[par], cq, rr, wave);
-      par ^= 1;
+      if constexpr (!RUST) {
+        cn_wave_sums(csum, red[par], cq, rr, wave);
+        par ^= 1;
+      }
       float ema[4] = {0.0f, 0.0f, 0.0f, 0.0f};
       {
         RowDiv cd[4];
@@ -3118,6 +3170,11 @@ __global__ __launch_bounds__(512, 1) void k_bonds_cn(BondArgs A) {
 // tile in registers and keeps the inputs of the next P epochs in flight
 // (a register ring refilled as each epoch is consumed), so the per-epoch HBM
 // latency is hidden behind P-1 epochs of work.
+// Yuma / Yuma2 (yumas.py:227-258, :341-372) run here too once the rank pass
+// has formed their bond column sums csb = Σ_v S·W_b (k_rank_s BCS): then
+// B = nan_to_num(S·W_b / csb) and the EMA are element-wise, and the scan
+// reads each miner's C and csb beside its incentive (Yuma2 keeps the
+// previous epoch's normalised W in registers as its W_prev).
 // ---------------------------------------------------------------------------
 // Block shape: BS threads over CB miners x (G = BS / (CB/4)) rows per pass,
 // R passes, i.e. a block owns G R rows x CB miners of the bond state; lane
@@ -3146,12 +3203,16 @@ __global__ __launch_bounds__(BS, 1) void k_bonds_elem(BondArgs A) {
   const bool reset_all = (pg.flags & YUMA_FLAG_RESET_ALL_COLUMNS) != 0;
   const float p_bond_alpha = pg.bond_alpha, p_omba = pg.one_minus_bond_alpha;
   const float p_maxint = pg.maxint, p_capacity_alpha = pg.capacity_alpha, p_decay_keep = pg.decay_keep;
+  const float p_pen = pg.bond_penalty, p_ompen = pg.one_minus_bond_penalty;
+  constexpr bool COLNORM = VARIANT == YUMA_VARIANT_YUMA1 || VARIANT == YUMA_VARIANT_YUMA2;
+  constexpr bool YUMA2 = VARIANT == YUMA_VARIANT_YUMA2;
+  static_assert(VARIANT != YUMA_VARIANT_RUST, "YumaRust renormalises B_ema over every validator (k_bonds_cn)");
   const int row0 = rb * G * R + g;
   // the conditional reset's test (C of the previous epoch at the reset
   // column), read before the epoch loop: a load in the loop's rare reset
   // branch made the waitcnt pass drain the whole prefetch ring (vmcnt(0))
-  // at every epoch, stores included
-  const bool zero_c = reset_c_zero(A, n, reset_mode, reset_all, reset_epoch, reset_index);
+  // at every epoch, stores included. Resets are Yuma 3.x / 4 only.
+  const bool zero_c = !COLNORM && reset_c_zero(A, n, reset_mode, reset_all, reset_epoch, reset_index);
 
   float B[R][4];
   bool has_old;
@@ -3168,8 +3229,44 @@ __global__ __launch_bounds__(BS, 1) void k_bonds_elem(BondArgs A) {
         for (int c = 0; c < 4; ++c) B[i][c] = 0.0f;
     }
   }
+  // Yuma2: the previous epoch's normalised weights (yumas.py:299-300, 328):
+  // the caller's W_prev at epoch 0 (none: W itself), else W[t0 - 1] / its row sums
+  float Wp[COLNORM ? R : 1][4];
+  bool have_wp = false;
+  if constexpr (YUMA2) {
+#pragma unroll
+    for (int i = 0; i < R; ++i)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) Wp[i][c] = 0.0f;
+    if (A.t0 == 0) {
+      if (A.Wprev_init != nullptr) {
+        have_wp = true;
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+          const int row = row0 + G * i;
+          if (row < V) load4<VEC>(A.Wprev_init + n * VM + (long long)row * M, m, M, Wp[i]);
+        }
+      }
+    } else {
+      have_wp = true;
+      const long long ps = (long long)(A.t0 - 1) * N + n;
+      const long long pw = A.wsh ? (long long)(A.t0 - 1) : ps;
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        const int row = row0 + G * i;
+        if (row < V) {
+          float x[4];
+          load4<VEC>(A.W + pw * VM + (long long)row * M, m, M, x);
+          const float d = A.rsd[ps * V + row];
+#pragma unroll
+          for (int c = 0; c < 4; ++c) Wp[i][c] = x[c] / d;
+        }
+      }
+    }
+  }
 
   float rw[P][R][4], rd[P][R], rsn[P][R], ri[P][4], rba[P][4];
+  float rcc[COLNORM ? P : 1][4], rcs[COLNORM ? P : 1][4];  // Yuma / Yuma2: C and csb
   // DP_QTE: the quad partials of up to kQBuf epochs parked in LDS (one float
   // per wave row and epoch) and written out as contiguous runs when the
   // buffer fills or the launch ends: no global store inside the epoch loop
@@ -3194,9 +3291,17 @@ __global__ __launch_bounds__(BS, 1) void k_bonds_elem(BondArgs A) {
     if (VECI) {
       load4c<true>(A.I + slice * M, 0, 1, m, M, ri[k]);
       if (liquid) load4c<true>(A.ba + slice * M, 0, 1, m, M, rba[k]);
+      if constexpr (COLNORM) {
+        load4c<true>(A.C + slice * M, 0, 1, m, M, rcc[k]);
+        load4c<true>(A.csb + slice * M, 0, 1, m, M, rcs[k]);
+      }
     } else {
       vec4raw(A.I + slice * M, m, M, ri[k]);
       if (liquid) vec4raw(A.ba + slice * M, m, M, rba[k]);
+      if constexpr (COLNORM) {
+        vec4raw(A.C + slice * M, m, M, rcc[k]);
+        vec4raw(A.csb + slice * M, m, M, rcs[k]);
+      }
     }
   };
 #pragma unroll
@@ -3209,7 +3314,7 @@ __global__ __launch_bounds__(BS, 1) void k_bonds_elem(BondArgs A) {
       const int t = tb + k;
       if (t >= A.t1) break;
       const long long slice = (long long)t * N + n;
-      if (has_old && reset_mode != YUMA_RESET_NONE && t == reset_epoch &&
+      if (!COLNORM && has_old && reset_mode != YUMA_RESET_NONE && t == reset_epoch &&
           (reset_all || (reset_index >= 0 && reset_index < M))) {
         bool fire = reset_mode == YUMA_RESET_ALWAYS;
         if (reset_mode == YUMA_RESET_IF_ZERO_CONSENSUS && t >= 1 && !reset_all) fire = zero_c;
@@ -3240,7 +3345,9 @@ __global__ __launch_bounds__(BS, 1) void k_bonds_elem(BondArgs A) {
         // (Yuma4 with the history stream keeps the compare/select forms:
         // same-box A/B, its scan ran 1.70 -> 1.81 ms with the short ones,
         // while Yuma3 gained 0.05 ms and the history-less c3 sweep 20 %.)
-        constexpr bool SHORT = !(VARIANT == YUMA_VARIANT_YUMA4 && NT);
+        // (Yuma / Yuma2 keep the sign-exact division and clip: there a
+        // -0 weight can reach the bond state as S·W_b = -0.)
+        constexpr bool SHORT = !COLNORM && !(VARIANT == YUMA_VARIANT_YUMA4 && NT);
         auto mn = [](float a, float b) { return SHORT ? vmin(a, b) : tmin(a, b); };
         auto mx = [](float a, float b) { return SHORT ? vmax(a, b) : tmax(a, b); };
         // (k_rowsum's screened reciprocal instead of the per-row one and the
@@ -3256,7 +3363,20 @@ __global__ __launch_bounds__(BS, 1) void k_bonds_elem(BondArgs A) {
 #pragma unroll
           for (int c = 0; c < 4; ++c) wn[c] = rw[k][i][c] / rd[k][i];
         }
-        if (VARIANT == YUMA_VARIANT_YUMA3) {
+        if constexpr (COLNORM) {
+          // B = nan_to_num(S·W_b / Σ_v S·W_b), W_b = (1-β)·src + β·min(src, C)
+          // (yumas.py:227-229; Yuma2 src = W_prev :341-343), then the EMA
+          // α·B + (1-α)·B_old, or B itself without a bond state (:255-258)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            const float src = (YUMA2 && have_wp) ? Wp[i][c] : wn[c];
+            const float wc = tmin(src, rcc[k][c]);
+            const float wb = p_ompen * src + p_pen * wc;
+            const float b = nan_to_num((rsn[k][i] * wb) / rcs[k][c], 0.0f);
+            B[i][c] = has_old ? bac[c] * b + omba[c] * B[i][c] : b;
+            if (YUMA2) Wp[i][c] = wn[c];
+          }
+        } else if (VARIANT == YUMA_VARIANT_YUMA3) {
           const float cap = rsn[k][i] * p_maxint;
           const float ca = p_capacity_alpha * cap;
 #pragma unroll
@@ -3330,6 +3450,7 @@ __global__ __launch_bounds__(BS, 1) void k_bonds_elem(BondArgs A) {
         }
       }
       has_old = true;
+      if (YUMA2) have_wp = true;
       if (t + P < A.t1) fetch(k, t + P);
     }
   }
@@ -3954,6 +4075,8 @@ struct Workspace {
   float* sumc_f;
   double* sumc_d;
   int* crep;  // per scenario: consensus class representative (k_classes)
+  int* rcrep;  // per scenario: rank class representative (Yuma: + bond_penalty)
+  float* csb;  // Yuma / Yuma2: [slice][M] Σ_v S·W_b (k_rank_s)
   size_t bytes;
 };
 
@@ -3998,11 +4121,22 @@ Workspace carve(char* base, int variant, int N, int E, int V, int M, int full) {
   w.sumc_f = (float*)take(S * 4);
   w.sumc_d = (double*)take(S * 8);
   w.crep = (int*)take((size_t)N * 4);
+  w.rcrep = (int*)take((size_t)N * 4);
+  w.csb = (variant == YUMA_VARIANT_YUMA1 || variant == YUMA_VARIANT_YUMA2) ? (float*)take(S * M * 4) : nullptr;
   w.bytes = off;
   return w;
 }
 
 bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+// k_incentive's float4 rows: M % 4 == 0 and every row buffer it touches
+// 16-byte aligned (R, I, and T / P when the trust is requested); a caller's
+// output tensor may be a view at any 4-byte offset
+int incentive_v4(int M, const float* R, const float* I, const yuma_outputs_t* out) {
+  if ((M & 3) != 0 || !aligned16(R) || !aligned16(I)) return 0;
+  if (out->P != nullptr && (!aligned16(out->P) || (out->T != nullptr && !aligned16(out->T)))) return 0;
+  return 1;
+}
 
 // Row-configuration of the column-resident kernels: NT threads, R rows each.
 enum RowCfg { RC_256_1, RC_256_4, RC_256_16, RC_1024_16 };
@@ -4050,9 +4184,12 @@ void launch_consensus(RowCfg rc, long long nblocks, hipStream_t st, const float*
       // kernel for exact-stake inputs (the histogram / bisection sums are
       // exact); for generic float stakes the two kernels' F sums may differ
       // in the last bit at a tie, inside the tie window the tests allow.
-      if (VEC && !wsh && P == nullptr)
-        YK_LAUNCH((yk::k_consensus_p<true>), nblocks, 256, st, W, rsd, sn, sx, prm, N, V, M, slice0, tiles,
+      if (VEC && !wsh && P == nullptr) {
+        constexpr int NP = yk::kConsPairs;
+        const long long nb = NP == 2 ? nblocks : nblocks / tiles * ((M + 31) / 32);
+        YK_LAUNCH((yk::k_consensus_p<true, NP>), nb, 128 * NP, st, W, rsd, sn, sx, prm, N, V, M, slice0, tiles,
                   craw, P, wsh, crep, rq4);
+      }
       else
         launch_consensus_w<16, VEC>(nblocks, st, W, rsd, sn, sx, prm, N, V, M, slice0, tiles, craw, P, wsh,
                                     crep);
@@ -4080,19 +4217,28 @@ void launch_consensus(RowCfg rc, long long nblocks, hipStream_t st, const float*
   }
 }
 
+// csb (streaming rank only, Yuma / Yuma2): also form the bond column sums
+// Σ_v S·W_b per slice and miner (k_rank_s BCS) for the element-wise bond scan
 template <bool VEC>
 void launch_rank(RowCfg rc, long long nblocks, hipStream_t st, const float* W, const float* rsd,
                  const float* sn, const float* C, const float* Wprev_init, int yuma2, int N,
                  int V, int M, long long slice0, int tiles, float* R, float* rpart, float* Wn,
-                 float* Wc, float* tvc, float* tvn, int wsh, const int* crep = nullptr) {
+                 float* Wc, float* tvc, float* tvn, int wsh, const int* crep = nullptr,
+                 float* csb = nullptr, const yuma_params_t* prm = nullptr) {
   const bool full = Wn != nullptr || Wc != nullptr || tvc != nullptr;
   if (!full) {  // streaming rank; k_rank_w also materialises Wn / Wc / T_v
-    if (yuma2)  // per scenario: W_prev (the caller's) is not shared by a consensus class
+    if (yuma2 && csb)  // per scenario: W_prev (the caller's) is not shared by a consensus class
+      YK_LAUNCH((yk::k_rank_s<VEC, true, true>), nblocks, 256, st, W, rsd, sn, C, N, V, M, slice0, tiles,
+                R, rpart, wsh, nullptr, Wprev_init, csb, prm);
+    else if (yuma2)
       YK_LAUNCH((yk::k_rank_s<VEC, true>), nblocks, 256, st, W, rsd, sn, C, N, V, M, slice0, tiles, R,
-                rpart, wsh, nullptr, Wprev_init);
+                rpart, wsh, nullptr, Wprev_init, nullptr, prm);
+    else if (csb)
+      YK_LAUNCH((yk::k_rank_s<VEC, false, true>), nblocks, 256, st, W, rsd, sn, C, N, V, M, slice0, tiles,
+                R, rpart, wsh, crep, nullptr, csb, prm);
     else
       YK_LAUNCH((yk::k_rank_s<VEC, false>), nblocks, 256, st, W, rsd, sn, C, N, V, M, slice0, tiles, R,
-                rpart, wsh, crep, nullptr);
+                rpart, wsh, crep, nullptr, nullptr, prm);
     return;
   }
   auto go = [&](auto kern) {
@@ -4154,7 +4300,16 @@ int launch_cn(hipStream_t st, yk::BondArgs& A, int* ptiles) {
   return yk::DP_TV;
 }
 template <int VARIANT, bool VEC>
+int launch_bonds_elem(hipStream_t st, yk::BondArgs& A);
+template <int VARIANT, bool VEC>
 int launch_bonds_colnorm(RowCfg rc, hipStream_t st, yk::BondArgs& A, int* ptiles) {
+  if constexpr (VARIANT != YUMA_VARIANT_RUST) {
+    // the rank pass formed the bond column sums: element-wise scan
+    if (A.csb != nullptr && A.Wb_out == nullptr && A.Binst_out == nullptr) {
+      *ptiles = A.tiles;
+      return launch_bonds_elem<VARIANT, VEC>(st, A);
+    }
+  }
   if constexpr (VEC) {
     if (A.V > 64 && A.Wb_out == nullptr && A.Binst_out == nullptr) {
       if (A.V <= 128) return launch_cn<VARIANT, 1>(st, A, ptiles);
@@ -4198,6 +4353,7 @@ int launch_bonds_colnorm(RowCfg rc, hipStream_t st, yk::BondArgs& A, int* ptiles
 // Sweeps over one shared input trajectory run k_bonds_grp with K = 4
 // scenarios per block (k_bonds_grp's history).
 constexpr int kWideP = 2;      // epochs in flight of the wide history scan
+constexpr int kWidePCn = 2;    // ... for Yuma / Yuma2 (more work per epoch)
 constexpr int kScanGroup = 4;  // scenarios per block of the shared-input scan
 int bonds_rows(bool vec, bool hist, bool wsh) { return vec && (hist || wsh) ? 2 : 1; }
 template <int VARIANT, int R, bool VEC, int P, bool VECI, bool NT, int BS, int CB, int DPL>
@@ -4214,9 +4370,10 @@ int launch_bonds_elem(hipStream_t st, yk::BondArgs& A) {
   const bool hist = A.B_hist != nullptr;
   if constexpr (VEC) {
     if (hist && A.M >= 1024)
-      return launch_elem_shape<VARIANT, 2, true, kWideP, true, true, 512, 1024, yk::DP_VQ>(st, A);
+      return launch_elem_shape<VARIANT, 2, true, VARIANT <= YUMA_VARIANT_YUMA2 ? kWidePCn : kWideP, true, true,
+                               512, 1024, yk::DP_VQ>(st, A);
   }
-  if constexpr (VEC) {
+  if constexpr (VEC && VARIANT >= YUMA_VARIANT_YUMA3) {
     if (A.wsh && A.N >= 2 && A.rq4 != nullptr) {  // a sweep over one input trajectory
       constexpr int K = kScanGroup, R = 2;
       A.rowblocks = (A.V + 16 * R - 1) / (16 * R);
@@ -4327,14 +4484,22 @@ int run_impl(int variant, const yuma_params_t* prm, int N, int E, int V, int M, 
   // (k_classes). Off when the prerank P is requested (the consensus pass
   // writes it for every slice) and for the materialising / Yuma2 rank.
   const int* crep = nullptr;
+  const long long ncb = (N + 255) / 256 < 64 ? (N + 255) / 256 : 64;
   if (wsh && N > 1 && out->P == nullptr) {
-    const long long nb = (N + 255) / 256;
-    YK_LAUNCH(yk::k_classes, nb < 64 ? nb : 64, 256, st, prm, N, ws.crep);
+    YK_LAUNCH(yk::k_classes, ncb, 256, st, prm, N, ws.crep, 0);
     crep = ws.crep;
   }
-  const bool rank_stream = out->Wn == nullptr && out->Wc == nullptr && ws.tvc == nullptr &&
-                           variant != YUMA_VARIANT_YUMA2;  // Yuma2's W_prev: rank per scenario
+  // Yuma / Yuma2 run outputs above 64 validators: the streaming rank also
+  // forms the bond column sums Σ_v S·W_b and the bond scan is element-wise
+  const bool streaming = out->Wn == nullptr && out->Wc == nullptr && ws.tvc == nullptr;
+  float* csb = (ws.csb != nullptr && streaming && V > 64 && out->Wb == nullptr && out->B_inst == nullptr)
+                   ? ws.csb : nullptr;
+  const bool rank_stream = streaming && variant != YUMA_VARIANT_YUMA2;  // Yuma2's W_prev: rank per scenario
   const int* rcrep = rank_stream ? crep : nullptr;
+  if (rcrep != nullptr && csb != nullptr) {  // the column sums depend on bond_penalty too
+    YK_LAUNCH(yk::k_classes, ncb, 256, st, prm, N, ws.rcrep, 1);
+    rcrep = ws.rcrep;
+  }
 
   PhaseTimer tm{};
   tm.ms = phase_ms;
@@ -4378,16 +4543,16 @@ int run_impl(int variant, const yuma_params_t* prm, int N, int E, int V, int M, 
       if (vec)
         launch_rank<true>(rc, ns * tiles, st, W, ws.rsd, ws.sn, C, Wprev_init,
                           variant == YUMA_VARIANT_YUMA2, N, V, M, s0, tiles, Rr, ws.rpart, out->Wn,
-                          out->Wc, ws.tvc, ws.tvn, wsh, rcrep);
+                          out->Wc, ws.tvc, ws.tvn, wsh, rcrep, csb, prm);
       else
         launch_rank<false>(rc, ns * tiles, st, W, ws.rsd, ws.sn, C, Wprev_init,
                            variant == YUMA_VARIANT_YUMA2, N, V, M, s0, tiles, Rr, ws.rpart,
-                           out->Wn, out->Wc, ws.tvc, ws.tvn, wsh, rcrep);
+                           out->Wn, out->Wc, ws.tvc, ws.tvn, wsh, rcrep, csb, prm);
     }
     tm.mark(YUMA_PHASE_INCENTIVE);
     const int ich = (M + yk::kIncCols - 1) / yk::kIncCols;
     YK_LAUNCH(yk::k_incentive, ns * ich, 256, st, Rr, ws.rpart, out->P, M, s0, tiles, I,
-              out->P ? out->T : nullptr, ws.scal, nullptr, rcrep, N, ich);
+              out->P ? out->T : nullptr, ws.scal, nullptr, rcrep, N, ich, incentive_v4(M, Rr, I, out));
 
     yk::BondArgs A{};
     A.W = W;
@@ -4405,6 +4570,8 @@ int run_impl(int variant, const yuma_params_t* prm, int N, int E, int V, int M, 
     A.Binst_out = out->B_inst;
     A.dpart = ws.dpart;
     A.rq4 = ws.rq4;
+    A.csb = csb;
+    A.R = Rr;
     A.N = N;
     A.V = V;
     A.M = M;
@@ -4496,6 +4663,11 @@ int shard_stage_impl(int stage, int variant, const yuma_params_t* prm, int N, in
   float* ba_buf = out->bond_alpha ? out->bond_alpha : ws.ba;
   int* qlev = io->levels ? io->levels : ws.qlev;
   const long long ns = (long long)E * N;
+  // Yuma / Yuma2: the bond column sums are sums over validators, local to
+  // the shard's columns: formed by stage 3's rank pass, read by stage 4's scan
+  float* shard_csb = (ws.csb != nullptr && !full && V > 64 && out->Wn == nullptr && out->Wc == nullptr &&
+                      out->Wb == nullptr && out->B_inst == nullptr)
+                         ? ws.csb : nullptr;
   switch (stage) {
     case 1: {
       if (!io->rowsum_part) return fail(YUMA_EINVAL, "stage 1 needs io->rowsum_part");
@@ -4532,11 +4704,11 @@ int shard_stage_impl(int stage, int variant, const yuma_params_t* prm, int N, in
       if (vec)
         launch_rank<true>(rc, ns * tiles, st, W, ws.rsd, ws.sn, C, Wprev_init,
                           variant == YUMA_VARIANT_YUMA2, N, V, M, 0LL, tiles, R, ws.rpart,
-                          out->Wn, out->Wc, ws.tvc, ws.tvn, 0);
+                          out->Wn, out->Wc, ws.tvc, ws.tvn, 0, nullptr, shard_csb, prm);
       else
         launch_rank<false>(rc, ns * tiles, st, W, ws.rsd, ws.sn, C, Wprev_init,
                            variant == YUMA_VARIANT_YUMA2, N, V, M, 0LL, tiles, R, ws.rpart,
-                           out->Wn, out->Wc, ws.tvc, ws.tvn, 0);
+                           out->Wn, out->Wc, ws.tvc, ws.tvn, 0, nullptr, shard_csb, prm);
       YK_LAUNCH(yk::k_rsum, ns, 64, st, ws.rpart, tiles, io->rsum_part);
       if (full) {
         YK_LAUNCH(yk::k_dsum, ns, 256, st, ws.tvc, V, tiles, io->tv_part);
@@ -4554,7 +4726,7 @@ int shard_stage_impl(int stage, int variant, const yuma_params_t* prm, int N, in
                 rust ? 1 : 0);
       const int ich = (M + yk::kIncCols - 1) / yk::kIncCols;
       YK_LAUNCH(yk::k_incentive, ns * ich, 256, st, R, ws.rpart, out->P, M, 0LL, tiles, I,
-                out->P ? out->T : nullptr, ws.scal, io->rsum, nullptr, N, ich);
+                out->P ? out->T : nullptr, ws.scal, io->rsum, nullptr, N, ich, incentive_v4(M, R, I, out));
       yk::BondArgs A{};
       A.W = W;
       A.rsd = ws.rsd;
@@ -4570,6 +4742,8 @@ int shard_stage_impl(int stage, int variant, const yuma_params_t* prm, int N, in
       A.Wb_out = out->Wb;
       A.Binst_out = out->B_inst;
       A.dpart = ws.dpart;
+      A.csb = shard_csb;
+      A.R = R;
       A.N = N;
       A.V = V;
       A.M = M;
