@@ -1880,7 +1880,11 @@ __global__ __launch_bounds__(256) void k_rank_w(
 // β·min(src, C) (yumas.py:227-228, :341-342; src = W, Yuma2's W_prev). They
 // depend on the epoch's inputs only, so the bond scan then runs element-wise
 // (k_bonds_elem) instead of reducing every column over all validators each
-// epoch. Same summation order as R.
+// epoch. Same summation order as R. Beside csb it stores csr[m] = RN(1 / csb)
+// when the column passes the fast-division screen (csb and every nonzero
+// |S·W_b| of the column in [2^-60, 2^60], as RowDiv's guard), else NaN: the
+// scan then divides by Markstein's correction with no per-element guard, and
+// its quotients are finite, so nan_to_num is the identity there.
 template <bool VEC, bool YUMA2 = false, bool BCS = false>
 __global__ __launch_bounds__(256, 1) void k_rank_s(const float* __restrict__ W,
                                                 const float* __restrict__ rsd,
@@ -1892,9 +1896,11 @@ __global__ __launch_bounds__(256, 1) void k_rank_s(const float* __restrict__ W,
                                                 const int* __restrict__ crep,
                                                 const float* __restrict__ Wprev_init,
                                                 float* __restrict__ csb,
+                                                float* __restrict__ csr,
                                                 const yuma_params_t* __restrict__ prm) {
   __shared__ float4 red[4][16];
   __shared__ float4 red2[BCS ? 4 : 1][16];
+  __shared__ unsigned smx[BCS ? 4 : 1][64], smn[BCS ? 4 : 1][64];
   const Lay L = lay();
   const long long slice = slice0 + blockIdx.x / tiles;
   const int tile = blockIdx.x % tiles;
@@ -1935,6 +1941,9 @@ __global__ __launch_bounds__(256, 1) void k_rank_s(const float* __restrict__ W,
   __syncthreads();
   float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
   float acb[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  // BCS screen: max of |y| and min of nonzero |y| as bit patterns (<< 1 drops
+  // the sign; - 1 sends a zero to the top of the min)
+  unsigned ymx[4] = {0u, 0u, 0u, 0u}, ymn[4] = {~0u, ~0u, ~0u, ~0u};
   constexpr int B = 8;
   for (int r0 = L.g; r0 < V; r0 += 16 * B) {
     float w[B][4], d[B], s[B];
@@ -1977,6 +1986,9 @@ __global__ __launch_bounds__(256, 1) void k_rank_s(const float* __restrict__ W,
         if (BCS) {
           const float y = s[i] * (p_ompen * w[i][c] + p_pen * wc);
           acb[c] = live ? acb[c] + y : acb[c];
+          const unsigned yb = __float_as_uint(y) << 1;
+          ymx[c] = live ? max(ymx[c], yb) : ymx[c];
+          ymn[c] = live ? min(ymn[c], yb - 1u) : ymn[c];
         }
       }
     }
@@ -1986,8 +1998,22 @@ __global__ __launch_bounds__(256, 1) void k_rank_s(const float* __restrict__ W,
   if (L.lane < 16) red[L.wave][L.c4] = make_float4(acc[0], acc[1], acc[2], acc[3]);
   if (BCS) {
 #pragma unroll
-    for (int c = 0; c < 4; ++c) acb[c] = sum_rowgroups(acb[c]);
-    if (L.lane < 16) red2[L.wave][L.c4] = make_float4(acb[0], acb[1], acb[2], acb[3]);
+    for (int c = 0; c < 4; ++c) {
+      acb[c] = sum_rowgroups(acb[c]);
+#pragma unroll
+      for (int o = 16; o <= 32; o <<= 1) {
+        ymx[c] = max(ymx[c], (unsigned)__shfl_xor((int)ymx[c], o, 64));
+        ymn[c] = min(ymn[c], (unsigned)__shfl_xor((int)ymn[c], o, 64));
+      }
+    }
+    if (L.lane < 16) {
+      red2[L.wave][L.c4] = make_float4(acb[0], acb[1], acb[2], acb[3]);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        smx[L.wave][L.c4 * 4 + c] = ymx[c];
+        smn[L.wave][L.c4 * 4 + c] = ymn[c];
+      }
+    }
   }
   __syncthreads();
   if (L.wave == 0) {
@@ -2004,10 +2030,21 @@ __global__ __launch_bounds__(256, 1) void k_rank_s(const float* __restrict__ W,
   } else if (BCS && L.wave == 1) {
     const float* rf = reinterpret_cast<const float*>(&red2[0][0]);
     float r = rf[L.lane];
+    unsigned mx = smx[0][L.lane], mn = smn[0][L.lane];
 #pragma unroll
-    for (int w = 1; w < 4; ++w) r = r + rf[w * 64 + L.lane];
+    for (int w = 1; w < 4; ++w) {
+      r = r + rf[w * 64 + L.lane];
+      mx = max(mx, smx[w][L.lane]);
+      mn = min(mn, smn[w][L.lane]);
+    }
     const int mg = tile * kTileM + L.lane;
-    if (mg < M) csb[slice * M + mg] = r;
+    const float ar = fabsf(r);
+    const bool ok = ar >= 0x1p-60f && ar <= 0x1p60f && mx <= (__float_as_uint(0x1p60f) << 1) &&
+                    (mn == ~0u || mn + 1u >= (__float_as_uint(0x1p-60f) << 1));
+    if (mg < M) {
+      csb[slice * M + mg] = r;
+      csr[slice * M + mg] = ok ? 1.0f / r : qnan();
+    }
   }
 }
 
@@ -2561,6 +2598,7 @@ struct BondArgs {
   float* dpart;
   const float4* rq4;  // per input slice and row {row sum, RN(1 / row sum) or NaN, stake, 0} (k_rowsum)
   const float* csb;   // Yuma / Yuma2: [slice][M] Σ_v S·W_b (k_rank_s), or null
+  const float* csr;   // ... RN(1 / csb) or NaN (the column fails the division screen)
   const float* R;     // [slice][M] rank R = Σ_v S·Wc (YumaRust's first bond column sum)
   int N, V, M, tiles, rowblocks, t0, t1;
   int wsh;      // every scenario reads input slice t (yuma_run_shared)
@@ -3266,7 +3304,7 @@ __global__ __launch_bounds__(BS, 1) void k_bonds_elem(BondArgs A) {
   }
 
   float rw[P][R][4], rd[P][R], rsn[P][R], ri[P][4], rba[P][4];
-  float rcc[COLNORM ? P : 1][4], rcs[COLNORM ? P : 1][4];  // Yuma / Yuma2: C and csb
+  float rcc[COLNORM ? P : 1][4], rcs[COLNORM ? P : 1][4], rcr[COLNORM ? P : 1][4];  // Yuma / Yuma2: C, csb, csr
   // DP_QTE: the quad partials of up to kQBuf epochs parked in LDS (one float
   // per wave row and epoch) and written out as contiguous runs when the
   // buffer fills or the launch ends: no global store inside the epoch loop
@@ -3294,6 +3332,7 @@ __global__ __launch_bounds__(BS, 1) void k_bonds_elem(BondArgs A) {
       if constexpr (COLNORM) {
         load4c<true>(A.C + slice * M, 0, 1, m, M, rcc[k]);
         load4c<true>(A.csb + slice * M, 0, 1, m, M, rcs[k]);
+        load4c<true>(A.csr + slice * M, 0, 1, m, M, rcr[k]);
       }
     } else {
       vec4raw(A.I + slice * M, m, M, ri[k]);
@@ -3301,6 +3340,7 @@ __global__ __launch_bounds__(BS, 1) void k_bonds_elem(BondArgs A) {
       if constexpr (COLNORM) {
         vec4raw(A.C + slice * M, m, M, rcc[k]);
         vec4raw(A.csb + slice * M, m, M, rcs[k]);
+        vec4raw(A.csr + slice * M, m, M, rcr[k]);
       }
     }
   };
@@ -3331,6 +3371,15 @@ __global__ __launch_bounds__(BS, 1) void k_bonds_elem(BondArgs A) {
       for (int c = 0; c < 4; ++c) {
         bac[c] = liquid ? rba[k][c] : p_bond_alpha;
         omba[c] = liquid ? 1.0f - rba[k][c] : p_omba;
+      }
+      // Yuma / Yuma2: every column of the wave passed the rank pass's
+      // division screen (csr not NaN): Markstein division, finite quotients
+      bool cfast = false;
+      if constexpr (COLNORM) {
+        bool ok = true;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) ok &= rcr[k][c] == rcr[k][c];
+        cfast = __all(ok);
       }
 #pragma unroll
       for (int i = 0; i < R; ++i) {
@@ -3367,13 +3416,32 @@ __global__ __launch_bounds__(BS, 1) void k_bonds_elem(BondArgs A) {
           // B = nan_to_num(S·W_b / Σ_v S·W_b), W_b = (1-β)·src + β·min(src, C)
           // (yumas.py:227-229; Yuma2 src = W_prev :341-343), then the EMA
           // α·B + (1-α)·B_old, or B itself without a bond state (:255-258)
+          // (min: C is a quantised level >= +0, so v_minimum's -0 < +0 order
+          // gives torch.min's bits)
+          float num[4], b[4];
 #pragma unroll
           for (int c = 0; c < 4; ++c) {
             const float src = (YUMA2 && have_wp) ? Wp[i][c] : wn[c];
-            const float wc = tmin(src, rcc[k][c]);
+            const float wc = vmin(src, rcc[k][c]);
             const float wb = p_ompen * src + p_pen * wc;
-            const float b = nan_to_num((rsn[k][i] * wb) / rcs[k][c], 0.0f);
-            B[i][c] = has_old ? bac[c] * b + omba[c] * B[i][c] : b;
+            num[c] = rsn[k][i] * wb;
+          }
+          if (cfast) {
+            // RN(num / csb) from RN(1 / csb) (RowDiv's correction; the screen
+            // bounds every operand), a zero numerator keeping its sign
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+              const float q = num[c] * rcr[k][c];
+              const float e = fmaf(-rcs[k][c], q, num[c]);
+              b[c] = num[c] == 0.0f ? q : fmaf(e, rcr[k][c], q);
+            }
+          } else {
+#pragma unroll
+            for (int c = 0; c < 4; ++c) b[c] = nan_to_num(num[c] / rcs[k][c], 0.0f);
+          }
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            B[i][c] = has_old ? bac[c] * b[c] + omba[c] * B[i][c] : b[c];
             if (YUMA2) Wp[i][c] = wn[c];
           }
         } else if (VARIANT == YUMA_VARIANT_YUMA3) {
@@ -3491,8 +3559,11 @@ __global__ __launch_bounds__(BS, 1) void k_bonds_elem(BondArgs A) {
 // (profiles/r04/ab_round3.txt, ab_round4.txt).
 // ---------------------------------------------------------------------------
 constexpr int kGrpWaves = 3;  // minimum waves per SIMD of the sweep scan
-template <int VARIANT, int K, int R, int P, bool LIQ>
+// LQ: 0 = every scenario of the block has a fixed bond_alpha (block-uniform
+// operands), 2 = every one is liquid (per-miner bond_alpha), 1 = mixed.
+template <int VARIANT, int K, int R, int P, int LQ, bool HIST>
 __device__ __forceinline__ void grp_scan(const BondArgs& A, unsigned liquid_mask) {
+  constexpr bool LIQ = LQ != 0;
   constexpr int G = 16;
   const Lay L = lay();
   const int tile = blockIdx.x % A.tiles;
@@ -3507,8 +3578,13 @@ __device__ __forceinline__ void grp_scan(const BondArgs& A, unsigned liquid_mask
   // every parameter read once into registers (a load inside the epoch loop
   // would wait on the prefetches, see k_bonds_elem)
   float p_ba[K], p_omba[K], p_maxint[K], p_ca[K], p_dk[K];
-  int p_rmode[K], p_repoch[K], p_rindex[K];
-  unsigned rall_mask = 0;
+  // bond resets (simulation_utils.py:62-88) decided before the epoch loop:
+  // p_repoch[k] = the epoch whose update starts from the reset state, or -1
+  // when scenario k's reset never fires in this launch (mode, index range,
+  // the conditional test on the previous epoch's C: reset_c_zero); rcols =
+  // the columns of this lane it zeroes, 4 bits per scenario
+  int p_repoch[K];
+  unsigned rcols = 0;
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     const yuma_params_t& pg = A.prm[min(n0 + k, N - 1)];
@@ -3517,17 +3593,17 @@ __device__ __forceinline__ void grp_scan(const BondArgs& A, unsigned liquid_mask
     p_maxint[k] = pg.maxint;
     p_ca[k] = pg.capacity_alpha;
     p_dk[k] = pg.decay_keep;
-    p_rmode[k] = pg.reset_mode;
-    p_repoch[k] = pg.reset_epoch;
-    p_rindex[k] = pg.reset_index;
-    if (pg.flags & YUMA_FLAG_RESET_ALL_COLUMNS) rall_mask |= 1u << k;
+    const int mode = pg.reset_mode, index = pg.reset_index;
+    const bool all = (pg.flags & YUMA_FLAG_RESET_ALL_COLUMNS) != 0;
+    bool fire = k < nk && mode != YUMA_RESET_NONE && (all || (index >= 0 && index < M));
+    if (mode == YUMA_RESET_IF_ZERO_CONSENSUS && pg.reset_epoch >= 1 && !all)
+      fire = fire && reset_c_zero(A, n0 + k, mode, all, pg.reset_epoch, index);
+    else if (mode != YUMA_RESET_ALWAYS)
+      fire = false;
+    p_repoch[k] = fire ? pg.reset_epoch : -1;
+    const int c = index - m;
+    if (fire) rcols |= (all ? 0xFu : (c >= 0 && c < 4 ? 1u << c : 0u)) << (4 * k);
   }
-  // the conditional resets' tests, read before the epoch loop (k_bonds_elem)
-  unsigned zc_mask = 0;
-#pragma unroll
-  for (int k = 0; k < K; ++k)
-    if (k < nk && reset_c_zero(A, n0 + k, p_rmode[k], (rall_mask >> k) & 1u, p_repoch[k], p_rindex[k]))
-      zc_mask |= 1u << k;
 
   float B[K][R][4];
   bool has_old;
@@ -3591,7 +3667,7 @@ __device__ __forceinline__ void grp_scan(const BondArgs& A, unsigned liquid_mask
   const float* fB[K];
   float* pD[K];  // this epoch's dividend partials
   float* pH[K];  // this epoch's bond history, if stored
-  const bool hist = A.B_hist != nullptr;
+  constexpr bool hist = HIST;
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     const long long s0 = (long long)A.t0 * N + min(n0 + k, N - 1);
@@ -3607,7 +3683,7 @@ __device__ __forceinline__ void grp_scan(const BondArgs& A, unsigned liquid_mask
       ri[k][1] = x.y;
       ri[k][2] = x.z;
       ri[k][3] = x.w;
-      if (LIQ && ((liquid_mask >> k) & 1u)) {
+      if (LQ == 2 || (LQ == 1 && ((liquid_mask >> k) & 1u))) {
         const float4 y = *reinterpret_cast<const float4*>(fB[k]);
         rba[k][0] = y.x;
         rba[k][1] = y.y;
@@ -3675,24 +3751,24 @@ __device__ __forceinline__ void grp_scan(const BondArgs& A, unsigned liquid_mask
 #pragma unroll
       for (int k = 0; k < K; ++k) {
         if (k >= nk) break;
-        const bool reset_all = (rall_mask >> k) & 1u;
-        const int reset_mode = p_rmode[k], reset_index = p_rindex[k];
-        if (__builtin_expect(t == p_repoch[k] && has_old && reset_mode != YUMA_RESET_NONE &&
-                                 (reset_all || (reset_index >= 0 && reset_index < M)), 0)) {
-          bool fire = reset_mode == YUMA_RESET_ALWAYS;
-          if (reset_mode == YUMA_RESET_IF_ZERO_CONSENSUS && t >= 1 && !reset_all) fire = (zc_mask >> k) & 1u;
-          const int c = reset_index - m;
-          if (fire && (reset_all || (c >= 0 && c < 4)))
+        if (__builtin_expect(t == p_repoch[k] && has_old, 0)) {
+          const unsigned cols = rcols >> (4 * k);
 #pragma unroll
-            for (int i = 0; i < R; ++i)
+          for (int i = 0; i < R; ++i)
 #pragma unroll
-              for (int cc = 0; cc < 4; ++cc)
-                if (reset_all || cc == c) B[k][i][cc] = 0.0f;
+            for (int cc = 0; cc < 4; ++cc)
+              if ((cols >> cc) & 1u) B[k][i][cc] = 0.0f;
         }
-        float bac[4], omba[4], ic[4];
+        // this epoch's incentive / bond_alpha are used in place; the next
+        // epoch's are fetched after the update (no register copies)
+        float bac[4], omba[4];
+        const float* ic = ri[k];
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
-          if (LIQ) {
+          if (LQ == 2) {  // every scenario liquid: omba = 1 - bond_alpha (yumas.py:256)
+            bac[c] = rba[k][c];
+            omba[c] = 1.0f - rba[k][c];
+          } else if (LQ == 1) {
             // rba holds bond_alpha for a fixed-alpha scenario; p_corr turns
             // 1 - rba into its (double-derived) one_minus_bond_alpha exactly
             // and is +0 for a liquid one (see the set-up above)
@@ -3702,9 +3778,7 @@ __device__ __forceinline__ void grp_scan(const BondArgs& A, unsigned liquid_mask
             bac[c] = p_ba[k];
             omba[c] = p_omba[k];
           }
-          ic[c] = ri[k][c];
         }
-        fetch_s(k, t + 1 < A.t1);
 #pragma unroll
         for (int i = 0; i < R; ++i) {
           const int row = row0 + G * i;
@@ -3738,6 +3812,7 @@ __device__ __forceinline__ void grp_scan(const BondArgs& A, unsigned liquid_mask
           d = wsum16(d);
           if (L.c4 == 0 && row < V) pD[k][G * i] = d;
         }
+        fetch_s(k, t + 1 < A.t1);
         pD[k] += sD;
         if (hist) pH[k] += sM * V;
       }
@@ -3755,17 +3830,20 @@ __device__ __forceinline__ void grp_scan(const BondArgs& A, unsigned liquid_mask
   }
 }
 
-template <int VARIANT, int K, int R, int P>
+template <int VARIANT, int K, int R, int P, bool HIST>
 __global__ __launch_bounds__(256, kGrpWaves) void k_bonds_grp(BondArgs A) {
   const int n0 = (blockIdx.x / (A.tiles * A.rowblocks)) * K;
   unsigned liquid_mask = 0;
 #pragma unroll
   for (int k = 0; k < K; ++k)
     if (n0 + k < A.N && A.prm[n0 + k].liquid_mode != YUMA_LIQUID_OFF) liquid_mask |= 1u << k;
-  if (VARIANT == YUMA_VARIANT_YUMA4 && liquid_mask != 0)  // block-uniform; Yuma3 has no bond_alpha
-    grp_scan<VARIANT, K, R, P, true>(A, liquid_mask);
+  const int nk = A.N - n0 < K ? A.N - n0 : K;
+  if (VARIANT == YUMA_VARIANT_YUMA4 && liquid_mask == (1u << nk) - 1u)  // block-uniform; Yuma3 has no bond_alpha
+    grp_scan<VARIANT, K, R, P, 2, HIST>(A, liquid_mask);
+  else if (VARIANT == YUMA_VARIANT_YUMA4 && liquid_mask != 0)
+    grp_scan<VARIANT, K, R, P, 1, HIST>(A, liquid_mask);
   else
-    grp_scan<VARIANT, K, R, P, false>(A, 0u);
+    grp_scan<VARIANT, K, R, P, 0, HIST>(A, 0u);
 }
 
 // ---------------------------------------------------------------------------
@@ -4077,6 +4155,7 @@ struct Workspace {
   int* crep;  // per scenario: consensus class representative (k_classes)
   int* rcrep;  // per scenario: rank class representative (Yuma: + bond_penalty)
   float* csb;  // Yuma / Yuma2: [slice][M] Σ_v S·W_b (k_rank_s)
+  float* csr;  // ... and RN(1 / csb) where the column passes the division screen, else NaN
   size_t bytes;
 };
 
@@ -4122,7 +4201,9 @@ Workspace carve(char* base, int variant, int N, int E, int V, int M, int full) {
   w.sumc_d = (double*)take(S * 8);
   w.crep = (int*)take((size_t)N * 4);
   w.rcrep = (int*)take((size_t)N * 4);
-  w.csb = (variant == YUMA_VARIANT_YUMA1 || variant == YUMA_VARIANT_YUMA2) ? (float*)take(S * M * 4) : nullptr;
+  const bool cn = variant == YUMA_VARIANT_YUMA1 || variant == YUMA_VARIANT_YUMA2;
+  w.csb = cn ? (float*)take(S * M * 4) : nullptr;
+  w.csr = cn ? (float*)take(S * M * 4) : nullptr;
   w.bytes = off;
   return w;
 }
@@ -4224,21 +4305,21 @@ void launch_rank(RowCfg rc, long long nblocks, hipStream_t st, const float* W, c
                  const float* sn, const float* C, const float* Wprev_init, int yuma2, int N,
                  int V, int M, long long slice0, int tiles, float* R, float* rpart, float* Wn,
                  float* Wc, float* tvc, float* tvn, int wsh, const int* crep = nullptr,
-                 float* csb = nullptr, const yuma_params_t* prm = nullptr) {
+                 float* csb = nullptr, float* csr = nullptr, const yuma_params_t* prm = nullptr) {
   const bool full = Wn != nullptr || Wc != nullptr || tvc != nullptr;
   if (!full) {  // streaming rank; k_rank_w also materialises Wn / Wc / T_v
     if (yuma2 && csb)  // per scenario: W_prev (the caller's) is not shared by a consensus class
       YK_LAUNCH((yk::k_rank_s<VEC, true, true>), nblocks, 256, st, W, rsd, sn, C, N, V, M, slice0, tiles,
-                R, rpart, wsh, nullptr, Wprev_init, csb, prm);
+                R, rpart, wsh, nullptr, Wprev_init, csb, csr, prm);
     else if (yuma2)
       YK_LAUNCH((yk::k_rank_s<VEC, true>), nblocks, 256, st, W, rsd, sn, C, N, V, M, slice0, tiles, R,
-                rpart, wsh, nullptr, Wprev_init, nullptr, prm);
+                rpart, wsh, nullptr, Wprev_init, nullptr, nullptr, prm);
     else if (csb)
       YK_LAUNCH((yk::k_rank_s<VEC, false, true>), nblocks, 256, st, W, rsd, sn, C, N, V, M, slice0, tiles,
-                R, rpart, wsh, crep, nullptr, csb, prm);
+                R, rpart, wsh, crep, nullptr, csb, csr, prm);
     else
       YK_LAUNCH((yk::k_rank_s<VEC, false>), nblocks, 256, st, W, rsd, sn, C, N, V, M, slice0, tiles, R,
-                rpart, wsh, crep, nullptr, nullptr, prm);
+                rpart, wsh, crep, nullptr, nullptr, nullptr, prm);
     return;
   }
   auto go = [&](auto kern) {
@@ -4379,7 +4460,10 @@ int launch_bonds_elem(hipStream_t st, yk::BondArgs& A) {
       A.rowblocks = (A.V + 16 * R - 1) / (16 * R);
       A.cblocks = A.tiles;
       const long long nblocks = (long long)((A.N + K - 1) / K) * A.rowblocks * A.tiles;
-      YK_LAUNCH((yk::k_bonds_grp<VARIANT, K, R, 2>), nblocks, 256, st, A);
+      if (hist)
+        YK_LAUNCH((yk::k_bonds_grp<VARIANT, K, R, 2, true>), nblocks, 256, st, A);
+      else
+        YK_LAUNCH((yk::k_bonds_grp<VARIANT, K, R, 2, false>), nblocks, 256, st, A);
       return yk::DP_TV;
     }
   }
@@ -4543,11 +4627,11 @@ int run_impl(int variant, const yuma_params_t* prm, int N, int E, int V, int M, 
       if (vec)
         launch_rank<true>(rc, ns * tiles, st, W, ws.rsd, ws.sn, C, Wprev_init,
                           variant == YUMA_VARIANT_YUMA2, N, V, M, s0, tiles, Rr, ws.rpart, out->Wn,
-                          out->Wc, ws.tvc, ws.tvn, wsh, rcrep, csb, prm);
+                          out->Wc, ws.tvc, ws.tvn, wsh, rcrep, csb, ws.csr, prm);
       else
         launch_rank<false>(rc, ns * tiles, st, W, ws.rsd, ws.sn, C, Wprev_init,
                            variant == YUMA_VARIANT_YUMA2, N, V, M, s0, tiles, Rr, ws.rpart,
-                           out->Wn, out->Wc, ws.tvc, ws.tvn, wsh, rcrep, csb, prm);
+                           out->Wn, out->Wc, ws.tvc, ws.tvn, wsh, rcrep, csb, ws.csr, prm);
     }
     tm.mark(YUMA_PHASE_INCENTIVE);
     const int ich = (M + yk::kIncCols - 1) / yk::kIncCols;
@@ -4571,6 +4655,7 @@ int run_impl(int variant, const yuma_params_t* prm, int N, int E, int V, int M, 
     A.dpart = ws.dpart;
     A.rq4 = ws.rq4;
     A.csb = csb;
+    A.csr = ws.csr;
     A.R = Rr;
     A.N = N;
     A.V = V;
@@ -4704,11 +4789,11 @@ int shard_stage_impl(int stage, int variant, const yuma_params_t* prm, int N, in
       if (vec)
         launch_rank<true>(rc, ns * tiles, st, W, ws.rsd, ws.sn, C, Wprev_init,
                           variant == YUMA_VARIANT_YUMA2, N, V, M, 0LL, tiles, R, ws.rpart,
-                          out->Wn, out->Wc, ws.tvc, ws.tvn, 0, nullptr, shard_csb, prm);
+                          out->Wn, out->Wc, ws.tvc, ws.tvn, 0, nullptr, shard_csb, ws.csr, prm);
       else
         launch_rank<false>(rc, ns * tiles, st, W, ws.rsd, ws.sn, C, Wprev_init,
                            variant == YUMA_VARIANT_YUMA2, N, V, M, 0LL, tiles, R, ws.rpart,
-                           out->Wn, out->Wc, ws.tvc, ws.tvn, 0, nullptr, shard_csb, prm);
+                           out->Wn, out->Wc, ws.tvc, ws.tvn, 0, nullptr, shard_csb, ws.csr, prm);
       YK_LAUNCH(yk::k_rsum, ns, 64, st, ws.rpart, tiles, io->rsum_part);
       if (full) {
         YK_LAUNCH(yk::k_dsum, ns, 256, st, ws.tvc, V, tiles, io->tv_part);
@@ -4743,6 +4828,7 @@ int shard_stage_impl(int stage, int variant, const yuma_params_t* prm, int N, in
       A.Binst_out = out->B_inst;
       A.dpart = ws.dpart;
       A.csb = shard_csb;
+      A.csr = ws.csr;
       A.R = R;
       A.N = N;
       A.V = V;
