@@ -280,3 +280,100 @@ def test_wide_local_strip_scan_matches_unsharded(name):
     got = wide.run_wide_local(variant, params, W, S, 3, want_hist=True)
     torch.cuda.synchronize()
     _compare(got, ref, wide.column_ranges(Mw, 3))
+
+
+def _gather4_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        g = wide.dist_gather()
+        widths = [3, 1, 4, 2]
+        x = torch.arange(2 * widths[rank], dtype=torch.int32).reshape(2, widths[rank]) + 1000 * rank
+        parts = g([x], widths)
+        q.put((rank, [p.numpy() for p in parts]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dist_gather_four_ranks_uneven():
+    """the padded all-gather with more than two ranks and
+    uneven last dimensions (int32, as the liquid-alpha level exchange)."""
+    world = 4
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gather4_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    widths = [3, 1, 4, 2]
+    for r in range(world):
+        for k in range(world):
+            exp = np.arange(2 * widths[k], dtype=np.int32).reshape(2, widths[k]) + 1000 * k
+            np.testing.assert_array_equal(got[r][k], exp)
+
+
+# c4's width plus three tiles: 1027 tiles cut into 257 + 257 + 257 + 256
+E4, V4, M4 = 3, 256, 65536 + 64 * 3
+
+
+def _c4_inputs():
+    W = engine.synth_weights(0x5EED0004, E4, 1, V4, M4)
+    S = torch.from_numpy(synth.stakes(0x5EED0004, E4, 1, V4, period=2)).to(W.device)
+    return W, S
+
+
+def _wide4_worker(rank, world, port, name, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        variant, par = CASES[name]
+        W, S = _c4_inputs()
+        params = _params(variant, par, 1)
+        cols = wide.column_ranges(M4, world)[rank]
+        res = wide.run_wide_distributed(variant, params, W[..., cols.start:cols.stop].contiguous(), S,
+                                        M_total=M4, want_hist=True)
+        torch.cuda.synchronize()
+        q.put((rank, res.Dn.cpu().numpy(), res.C[0].cpu().numpy(), res.I[0].cpu().numpy(),
+               res.B_hist[0].cpu().numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["yuma4_liquid", "yuma1"])
+def test_wide_distributed_four_ranks_uneven(name):
+    """c4's wide subnet (256 x 65728: uneven shards) over
+    four gloo ranks sharing the GPU — the padded dist_gather, the liquid-alpha
+    level exchange and the shard-ordered sums with more than two ranks —
+    bitwise equal to run_wide_local(..., 4) (the same stages and shard-order
+    sums in one process); yuma1 runs its element-wise bond scan on the rank
+    pass's column sums inside each shard."""
+    world = 4
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_wide4_worker, args=(r, world, port, name, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = {}
+    for _ in procs:
+        r, *vals = q.get(timeout=200)
+        got[r] = vals
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    variant, par = CASES[name]
+    W, S = _c4_inputs()
+    cols = wide.column_ranges(M4, world)
+    assert len({len(c) for c in cols}) == 2  # uneven shards
+    ref = wide.run_wide_local(variant, _params(variant, par, 1), W, S, world, want_hist=True)
+    torch.cuda.synchronize()
+    for r in range(world):
+        np.testing.assert_array_equal(got[r][0], ref.Dn.cpu().numpy())  # every rank: the same dividends
+        np.testing.assert_array_equal(got[r][1], ref.C[r].cpu().numpy())
+        np.testing.assert_array_equal(got[r][2], ref.I[r].cpu().numpy())
+        np.testing.assert_array_equal(got[r][3], ref.B_hist[r].cpu().numpy())

@@ -228,3 +228,8 @@ PATCHES["cn_rcp"] = [(
           }""")]
 PATCHES["cn_rcp_p3"] = PATCHES["cn_rcp"] + PATCHES["cn_p3"]
 PATCHES["cn_vmin_p3"] = PATCHES["cn_vmin"] + PATCHES["cn_p3"]
+PATCHES["cons_w4"] = [("__global__ __launch_bounds__(128 * NP, 3) void k_consensus_p", "__global__ __launch_bounds__(128 * NP, 4) void k_consensus_p")]
+PATCHES["rank_narrow"] = [("constexpr int kRankWide = 1;", "constexpr int kRankWide = 0;")]
+# (scan_rowvec / kScanRowUniform: wave-uniform scalar row-sum / stake loads in
+# the one-row-per-wave scans, c4 bonds 1.377-1.391 against 1.395-1.402 with
+# vector loads: rejected and removed, profiles/r05/ab_c4_rowuniform.txt)

@@ -1986,9 +1986,10 @@ __global__ __launch_bounds__(256, 1) void k_rank_s(const float* __restrict__ W,
         if (BCS) {
           const float y = s[i] * (p_ompen * w[i][c] + p_pen * wc);
           acb[c] = live ? acb[c] + y : acb[c];
+          // (a padding row repeats row V - 1: no mask needed for max / min)
           const unsigned yb = __float_as_uint(y) << 1;
-          ymx[c] = live ? max(ymx[c], yb) : ymx[c];
-          ymn[c] = live ? min(ymn[c], yb - 1u) : ymn[c];
+          ymx[c] = max(ymx[c], yb);
+          ymn[c] = min(ymn[c], yb - 1u);
         }
       }
     }
@@ -2044,6 +2045,156 @@ __global__ __launch_bounds__(256, 1) void k_rank_s(const float* __restrict__ W,
     if (mg < M) {
       csb[slice * M + mg] = r;
       csr[slice * M + mg] = ok ? 1.0f / r : qnan();
+    }
+  }
+}
+
+// k_rank_s on wide column blocks: a block owns 256 miners (four tiles) of
+// every row, a wave instruction moves one row's 1 KiB (the bond scan's and
+// the row sums' footprint, tools/scanbw), wave w streams rows w, w + 4, ...
+// in batches of 8 loads per lane. Order: rows sequentially per lane, then the
+// 4 waves in order (LDS); tile partials as k_rank_s (the 64 miners of a tile
+// by the wave butterfly). Same outputs and options as k_rank_s. Launched for
+// the ranks that also form Yuma / Yuma2's bond column sums (BCS): there it
+// takes 0.75 ms at c2 against 0.79 for k_rank_s; the plain rank is a tie
+// (0.70-0.72 against 0.70, profiles/r05/ab_rank_wide.txt), so k_rank_s stays.
+constexpr int kRankWide = 1;  // launch the wide form for BCS ranks (0: k_rank_s)
+template <bool VEC, bool YUMA2 = false, bool BCS = false>
+__global__ __launch_bounds__(256, 1) void k_rank_sw(const float* __restrict__ W,
+                                                 const float* __restrict__ rsd,
+                                                 const float* __restrict__ sn,
+                                                 const float* __restrict__ C, int N, int V, int M,
+                                                 long long slice0, int tiles,
+                                                 float* __restrict__ Rout,
+                                                 float* __restrict__ rpart, int wsh,
+                                                 const int* __restrict__ crep,
+                                                 const float* __restrict__ Wprev_init,
+                                                 float* __restrict__ csb,
+                                                 float* __restrict__ csr,
+                                                 const yuma_params_t* __restrict__ prm) {
+  constexpr int CB = 256;
+  __shared__ float red[4][CB];
+  __shared__ float red2[BCS ? 4 : 1][CB];
+  __shared__ unsigned smx[BCS ? 4 : 1][CB], smn[BCS ? 4 : 1][CB];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int cblocks = (M + CB - 1) / CB;
+  const long long slice = slice0 + blockIdx.x / cblocks;
+  const int cb = blockIdx.x % cblocks;
+  if (dup_slice(crep, slice, N)) return;  // block-uniform
+  float p_pen = 0.0f, p_ompen = 0.0f;
+  if (BCS) {
+    const yuma_params_t& pg = prm[slice % N];
+    p_pen = pg.bond_penalty;
+    p_ompen = pg.one_minus_bond_penalty;
+  }
+  const long long VM = (long long)V * M;
+  const int m = cb * CB + lane * 4;
+  long long wsl = slice;
+  bool divide = true;
+  const float* Ws = W + in_slice(slice, N, wsh) * VM;
+  if (YUMA2) {
+    if (slice >= N) {
+      wsl = slice - N;
+      Ws = W + in_slice(wsl, N, wsh) * VM;
+    } else if (Wprev_init != nullptr) {
+      Ws = Wprev_init + (slice % N) * VM;  // already normalised
+      divide = false;
+    }
+  }
+  float Cc[4];
+  load4c<VEC>(C + slice * M, 0, 1, m, M, Cc);
+  __shared__ float rows_d[YUMA_MAX_VALIDATORS], rows_r[YUMA_MAX_VALIDATORS], rows_s[YUMA_MAX_VALIDATORS];
+  for (int j = threadIdx.x; j < V; j += 256) {
+    const float dj = rsd[wsl * V + j];
+    rows_d[j] = dj;
+    rows_r[j] = 1.0f / dj;
+    rows_s[j] = sn[slice * V + j];
+  }
+  __syncthreads();
+  float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  float acb[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  unsigned ymx[4] = {0u, 0u, 0u, 0u}, ymn[4] = {~0u, ~0u, ~0u, ~0u};
+  constexpr int B = 8;
+  for (int r0 = wave; r0 < V; r0 += 4 * B) {
+    float w[B][4], d[B], s[B];
+#pragma unroll
+    for (int i = 0; i < B; ++i) {
+      const int rr = min(r0 + 4 * i, V - 1);
+      load4c<VEC>(Ws, rr, V, m, M, w[i]);
+      d[i] = rows_d[rr];
+      s[i] = rows_s[rr];
+    }
+    if (!YUMA2 || divide) {
+      bool slow = false;
+#pragma unroll
+      for (int i = 0; i < B; ++i) {
+        const int rr = min(r0 + 4 * i, V - 1);
+        const float ad = fabsf(d[i]);
+        const RowDiv rdv{d[i], rows_r[rr], ad >= 0x1p-60f && ad <= 0x1p60f};
+#pragma unroll
+        for (int c = 0; c < 4; ++c) w[i][c] = div_fast_nz(w[i][c], rdv, slow);
+      }
+      if (__any(slow)) {  // rare: redo the batch with IEEE division (wave-uniform)
+#pragma unroll
+        for (int i = 0; i < B; ++i) {
+          const int rr = min(r0 + 4 * i, V - 1);
+          float x[4];
+          load4c<VEC>(Ws, rr, V, m, M, x);
+#pragma unroll
+          for (int c = 0; c < 4; ++c) w[i][c] = x[c] / d[i];
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < B; ++i) {
+      const bool live = r0 + 4 * i < V;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const float wc = vmin(w[i][c], Cc[c]);
+        const float x = s[i] * wc;
+        acc[c] = live ? acc[c] + x : acc[c];
+        if (BCS) {
+          const float y = s[i] * (p_ompen * w[i][c] + p_pen * wc);
+          acb[c] = live ? acb[c] + y : acb[c];
+          // (a padding row repeats row V - 1: no mask needed for max / min)
+          const unsigned yb = __float_as_uint(y) << 1;
+          ymx[c] = max(ymx[c], yb);
+          ymn[c] = min(ymn[c], yb - 1u);
+        }
+      }
+    }
+  }
+  *reinterpret_cast<float4*>(&red[wave][lane * 4]) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+  if (BCS) {
+    *reinterpret_cast<float4*>(&red2[wave][lane * 4]) = make_float4(acb[0], acb[1], acb[2], acb[3]);
+    *reinterpret_cast<uint4*>(&smx[wave][lane * 4]) = make_uint4(ymx[0], ymx[1], ymx[2], ymx[3]);
+    *reinterpret_cast<uint4*>(&smn[wave][lane * 4]) = make_uint4(ymn[0], ymn[1], ymn[2], ymn[3]);
+  }
+  __syncthreads();
+  // wave w: tile 4 cb + w, lane l its miner l
+  const int j = wave * 64 + lane, mg = cb * CB + j, tile = cb * 4 + wave;
+  float r = red[0][j];
+#pragma unroll
+  for (int w = 1; w < 4; ++w) r = r + red[w][j];
+  if (mg < M) Rout[slice * M + mg] = r;
+  float t = mg < M ? r : 0.0f;
+  t = wave_sum(t);
+  if (lane == 0 && tile < tiles) rpart[slice * tiles + tile] = t;
+  if (BCS) {
+    float b = red2[0][j];
+    unsigned mx = smx[0][j], mn = smn[0][j];
+#pragma unroll
+    for (int w = 1; w < 4; ++w) {
+      b = b + red2[w][j];
+      mx = max(mx, smx[w][j]);
+      mn = min(mn, smn[w][j]);
+    }
+    const float ab = fabsf(b);
+    const bool ok = ab >= 0x1p-60f && ab <= 0x1p60f && mx <= (__float_as_uint(0x1p60f) << 1) &&
+                    (mn == ~0u || mn + 1u >= (__float_as_uint(0x1p-60f) << 1));
+    if (mg < M) {
+      csb[slice * M + mg] = b;
+      csr[slice * M + mg] = ok ? 1.0f / b : qnan();
     }
   }
 }
@@ -4307,6 +4458,22 @@ void launch_rank(RowCfg rc, long long nblocks, hipStream_t st, const float* W, c
                  float* Wc, float* tvc, float* tvn, int wsh, const int* crep = nullptr,
                  float* csb = nullptr, float* csr = nullptr, const yuma_params_t* prm = nullptr) {
   const bool full = Wn != nullptr || Wc != nullptr || tvc != nullptr;
+  if (!full && csb && yk::kRankWide) {  // streaming rank + bond column sums on 256-miner column blocks
+    const long long nb = nblocks / tiles * ((M + 255) / 256);
+    if (yuma2 && csb)
+      YK_LAUNCH((yk::k_rank_sw<VEC, true, true>), nb, 256, st, W, rsd, sn, C, N, V, M, slice0, tiles,
+                R, rpart, wsh, nullptr, Wprev_init, csb, csr, prm);
+    else if (yuma2)
+      YK_LAUNCH((yk::k_rank_sw<VEC, true>), nb, 256, st, W, rsd, sn, C, N, V, M, slice0, tiles, R,
+                rpart, wsh, nullptr, Wprev_init, nullptr, nullptr, prm);
+    else if (csb)
+      YK_LAUNCH((yk::k_rank_sw<VEC, false, true>), nb, 256, st, W, rsd, sn, C, N, V, M, slice0, tiles,
+                R, rpart, wsh, crep, nullptr, csb, csr, prm);
+    else
+      YK_LAUNCH((yk::k_rank_sw<VEC, false>), nb, 256, st, W, rsd, sn, C, N, V, M, slice0, tiles, R,
+                rpart, wsh, crep, nullptr, nullptr, nullptr, prm);
+    return;
+  }
   if (!full) {  // streaming rank; k_rank_w also materialises Wn / Wc / T_v
     if (yuma2 && csb)  // per scenario: W_prev (the caller's) is not shared by a consensus class
       YK_LAUNCH((yk::k_rank_s<VEC, true, true>), nblocks, 256, st, W, rsd, sn, C, N, V, M, slice0, tiles,
