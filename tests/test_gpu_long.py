@@ -151,3 +151,44 @@ def test_c3_full_trajectory_subset():
         np.testing.assert_array_equal(got["C"][:, j].cpu().numpy(), ref["C"], err_msg=tag)
         assert_close(got["Dn"][:, j].cpu().numpy(), ref["Dn"], what=f"{tag} Dn")
         assert_close(got["B_final"][j].cpu().numpy(), ref["B"][-1], what=f"{tag} B_final")
+
+
+@pytest.mark.parametrize("variant,liquid,N,chunk", [
+    (engine.VARIANT_YUMA4, "all", 8, 0),
+    (engine.VARIANT_YUMA4, "odd", 7, 23),
+    (engine.VARIANT_YUMA3, "none", 6, 0),
+])
+def test_sweep_scan_past_the_partial_flush(variant, liquid, N, chunk):
+    """The sweep scan (k_bonds_grp, shared inputs) parks its dividend
+    partials per wave in LDS and writes them every 32 epochs (kGrpDB): 75
+    epochs, one chunk and a 23-epoch chunk (flushes that do not start on a
+    multiple of 32), every liquid form of a block (all liquid / mixed /
+    fixed). Bitwise the results of the replicated run, whose history-less
+    scan stores its partials in another layout (the canonical sum is the
+    same); scenario 0 against the oracle (yumas.py:452-476, :570-593)."""
+    E, V, M = 75, 64, 512
+    seed = 0x5EED0075
+    W = engine.synth_weights(seed, E, 1, V, M)
+    S = torch.from_numpy(synth.stakes(seed, E, 1, V, period=20)).to(W.device)
+    cfgs = []
+    for i in range(N):
+        liq = liquid == "all" or (liquid == "odd" and i % 2 == 1)
+        cfgs.append(YumaConfig(simulation=bench_sim(kappa=0.35 + 0.1 * (i % 3)),
+                               yuma_params=YumaParams(bond_alpha=0.05 + 0.04 * i, liquid_alpha=liq)))
+    params = [engine.make_params(variant, c) for c in cfgs]
+    a = engine.run(variant, params, W, S, want_hist=False, chunk_epochs=chunk, shared_inputs=True)
+    b = engine.run(variant, params, W.expand(E, N, V, M).contiguous(), S.expand(E, N, V).contiguous(),
+                   want_hist=False, chunk_epochs=chunk)
+    torch.cuda.synchronize()
+    _equal_fields(a, b, ("C", "Dn", "I", "B_final"), f"sweep {liquid} chunk={chunk}")
+    version = "Yuma 3 (Rhef)" if variant == engine.VARIANT_YUMA3 else "Yuma 4 (Rhef+relative bonds)"
+    ref = orc.run(version, W[:, 0].cpu().numpy(), S[:, 0].cpu().numpy(), cfgs[0])
+    np.testing.assert_array_equal(a.C[:, 0].cpu().numpy(), ref["C"])
+    assert_close(a.Dn[:, 0].cpu().numpy(), ref["Dn"], what="Dn")
+    assert_close(a.B_final[0].cpu().numpy(), ref["B"][-1], what="B_final")
+
+
+def bench_sim(**kw):
+    from yuma_simulation._internal.yumas import SimulationHyperparameters
+
+    return SimulationHyperparameters(**kw)

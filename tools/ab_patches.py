@@ -233,3 +233,25 @@ PATCHES["rank_narrow"] = [("constexpr int kRankWide = 1;", "constexpr int kRankW
 # (scan_rowvec / kScanRowUniform: wave-uniform scalar row-sum / stake loads in
 # the one-row-per-wave scans, c4 bonds 1.377-1.391 against 1.395-1.402 with
 # vector loads: rejected and removed, profiles/r05/ab_c4_rowuniform.txt)
+
+# round 5: the plain streaming rank (k_rank_s, c2 Yuma 3): batch depth and
+# non-temporal loads
+PATCHES["rank_b4"] = [("  constexpr int B = 8;\n  for (int r0 = L.g; r0 < V; r0 += 16 * B) {",
+                       "  constexpr int B = 4;\n  for (int r0 = L.g; r0 < V; r0 += 16 * B) {")]
+PATCHES["rank_b16"] = [("  constexpr int B = 8;\n  for (int r0 = L.g; r0 < V; r0 += 16 * B) {",
+                        "  constexpr int B = 16;\n  for (int r0 = L.g; r0 < V; r0 += 16 * B) {")]
+PATCHES["rank_nt"] = [("      const int rr = min(r0 + 16 * i, V - 1);\n      load4c<VEC>(Ws, rr, V, m, M, w[i]);",
+                       "      const int rr = min(r0 + 16 * i, V - 1);\n      load4c<VEC, true>(Ws, rr, V, m, M, w[i]);")]
+PATCHES["rankw_plain"] = [("  if (!full && csb && yk::kRankWide) {", "  if (!full && yk::kRankWide) {")]
+
+# round 5: sweep scan, W ring refill issued after the epoch's per-scenario
+# incentive loads (vmcnt is in issue order: waiting for the next epoch's
+# incentive then no longer waits for the W rows two epochs ahead)
+PATCHES["grp_wlate"] = [
+    ("      fetch(kk, t + P < A.t1);\n#pragma unroll\n      for (int k = 0; k < K; ++k) {\n        if (k >= nk) break;",
+     "#pragma unroll\n      for (int k = 0; k < K; ++k) {\n        if (k >= nk) break;"),
+    ("      has_old = true;\n    }\n  }\n#pragma unroll\n  for (int k = 0; k < K; ++k) {\n    if (k >= nk) break;",
+     "      fetch(kk, t + P < A.t1);\n      has_old = true;\n    }\n  }\n#pragma unroll\n  for (int k = 0; k < K; ++k) {\n    if (k >= nk) break;")]
+PATCHES["grp_wlate_w4"] = PATCHES["grp_wlate"] + [("constexpr int kGrpWaves = 3;", "constexpr int kGrpWaves = 4;")]
+PATCHES["grp_nopark"] = [("constexpr bool kGrpPark = true;", "constexpr bool kGrpPark = false;")]
+PATCHES["grp_db16"] = [("constexpr int kGrpDB = 32;", "constexpr int kGrpDB = 16;")]

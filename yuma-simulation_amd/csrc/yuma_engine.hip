@@ -3710,10 +3710,12 @@ __global__ __launch_bounds__(BS, 1) void k_bonds_elem(BondArgs A) {
 // (profiles/r04/ab_round3.txt, ab_round4.txt).
 // ---------------------------------------------------------------------------
 constexpr int kGrpWaves = 3;  // minimum waves per SIMD of the sweep scan
+constexpr bool kGrpPark = true;  // dividend partials parked per wave in LDS
+constexpr int kGrpDB = 32;       // ... epochs per flush
 // LQ: 0 = every scenario of the block has a fixed bond_alpha (block-uniform
 // operands), 2 = every one is liquid (per-miner bond_alpha), 1 = mixed.
 template <int VARIANT, int K, int R, int P, int LQ, bool HIST>
-__device__ __forceinline__ void grp_scan(const BondArgs& A, unsigned liquid_mask) {
+__device__ __forceinline__ void grp_scan(const BondArgs& A, unsigned liquid_mask, float* dpark) {
   constexpr bool LIQ = LQ != 0;
   constexpr int G = 16;
   const Lay L = lay();
@@ -3867,6 +3869,36 @@ __device__ __forceinline__ void grp_scan(const BondArgs& A, unsigned liquid_mask
     }
   }
 
+  // Dividend partials parked per wave in LDS (kGrpDB epochs x K scenarios x R
+  // rows x the wave's 4 row groups) and written out as 16-byte row runs when
+  // the buffer fills or the launch ends: no global store in the epoch loop
+  // and no block barrier (a block-wide version lost in round 4)
+  float* dpb = dpark + (kGrpPark ? L.wave * (kGrpDB * K * R * 4) : 0);
+  int tq = A.t0;  // first epoch held in the wave's buffer
+  auto flush_d = [&](int t) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int rw0 = rb * G * R + L.wave * 4;  // this wave's first row of row-set i = 0
+    const int ne = (t - tq + 1) * K * R;
+    for (int j = L.lane; j < ne; j += 64) {
+      const int i = j % R, k = (j / R) % K, e = j / (R * K);
+      if (k >= nk) continue;
+      const int r = rw0 + G * i;
+      float* dst = A.dpart + (((long long)(tq + e) * N + n0 + k) * A.tiles + tile) * V + r;
+      const float* src = dpb + j * 4;
+      if ((V & 3) == 0 && r + 3 < V) {
+        *reinterpret_cast<float4*>(dst) = *reinterpret_cast<const float4*>(src);
+      } else {
+        for (int q = 0; q < 4; ++q)
+          if (r + q < V) dst[q] = src[q];
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    tq = t + 1;
+  };
   for (int tb = A.t0; tb < A.t1; tb += P) {
 #pragma unroll
     for (int kk = 0; kk < P; ++kk) {
@@ -3898,7 +3930,6 @@ __device__ __forceinline__ void grp_scan(const BondArgs& A, unsigned liquid_mask
       float sv[R];
 #pragma unroll
       for (int i = 0; i < R; ++i) sv[i] = rsn[kk][i];
-      fetch(kk, t + P < A.t1);
 #pragma unroll
       for (int k = 0; k < K; ++k) {
         if (k >= nk) break;
@@ -3961,11 +3992,23 @@ __device__ __forceinline__ void grp_scan(const BondArgs& A, unsigned liquid_mask
 #pragma unroll
             for (int c = 0; c < 4; ++c) d = d + B[k][i][c] * ic[c];
           d = wsum16(d);
-          if (L.c4 == 0 && row < V) pD[k][G * i] = d;
+          if constexpr (kGrpPark) {
+            if (L.c4 == 0) dpb[(((t - tq) * K + k) * R + i) * 4 + (L.lane >> 4)] = d;
+          } else {
+            if (L.c4 == 0 && row < V) pD[k][G * i] = d;
+          }
         }
         fetch_s(k, t + 1 < A.t1);
         pD[k] += sD;
         if (hist) pH[k] += sM * V;
+      }
+      // the W ring refill after this epoch's per-scenario incentive loads:
+      // vmcnt drains in issue order, so waiting for the next epoch's
+      // incentive does not wait for the rows two epochs ahead (c3 bonds
+      // 6.69-6.73 -> 6.61-6.62 ms, profiles/r05/ab_grp.txt)
+      fetch(kk, t + P < A.t1);
+      if constexpr (kGrpPark) {
+        if (t - tq == kGrpDB - 1 || t == A.t1 - 1) flush_d(t);  // wave-uniform
       }
       has_old = true;
     }
@@ -3983,6 +4026,7 @@ __device__ __forceinline__ void grp_scan(const BondArgs& A, unsigned liquid_mask
 
 template <int VARIANT, int K, int R, int P, bool HIST>
 __global__ __launch_bounds__(256, kGrpWaves) void k_bonds_grp(BondArgs A) {
+  __shared__ float dpark[kGrpPark ? 4 * kGrpDB * K * R * 4 : 1];
   const int n0 = (blockIdx.x / (A.tiles * A.rowblocks)) * K;
   unsigned liquid_mask = 0;
 #pragma unroll
@@ -3990,11 +4034,11 @@ __global__ __launch_bounds__(256, kGrpWaves) void k_bonds_grp(BondArgs A) {
     if (n0 + k < A.N && A.prm[n0 + k].liquid_mode != YUMA_LIQUID_OFF) liquid_mask |= 1u << k;
   const int nk = A.N - n0 < K ? A.N - n0 : K;
   if (VARIANT == YUMA_VARIANT_YUMA4 && liquid_mask == (1u << nk) - 1u)  // block-uniform; Yuma3 has no bond_alpha
-    grp_scan<VARIANT, K, R, P, 2, HIST>(A, liquid_mask);
+    grp_scan<VARIANT, K, R, P, 2, HIST>(A, liquid_mask, dpark);
   else if (VARIANT == YUMA_VARIANT_YUMA4 && liquid_mask != 0)
-    grp_scan<VARIANT, K, R, P, 1, HIST>(A, liquid_mask);
+    grp_scan<VARIANT, K, R, P, 1, HIST>(A, liquid_mask, dpark);
   else
-    grp_scan<VARIANT, K, R, P, 0, HIST>(A, 0u);
+    grp_scan<VARIANT, K, R, P, 0, HIST>(A, 0u, dpark);
 }
 
 // ---------------------------------------------------------------------------
