@@ -255,3 +255,18 @@ PATCHES["grp_wlate"] = [
 PATCHES["grp_wlate_w4"] = PATCHES["grp_wlate"] + [("constexpr int kGrpWaves = 3;", "constexpr int kGrpWaves = 4;")]
 PATCHES["grp_nopark"] = [("constexpr bool kGrpPark = true;", "constexpr bool kGrpPark = false;")]
 PATCHES["grp_db16"] = [("constexpr int kGrpDB = 32;", "constexpr int kGrpDB = 16;")]
+
+# round 5: the wide history scan parks its quad partials in LDS as the
+# history-less scan does (DP_QTE, k_dte_sum) instead of storing them per epoch
+PATCHES["hist_qte"] = [("                               512, 1024, yk::DP_VQ>(st, A);", "                               512, 1024, yk::DP_QTE>(st, A);")]
+# (hist_qte: c2 Yuma 3 bonds 1.560/1.535 -> 1.552/1.549, finalize + k_dte_sum
+# 0.008 -> 0.013-0.015 ms; Yuma 1 bonds 1.765 -> 1.74: a wash, rejected,
+# profiles/r05/ab_hist_qte.txt)
+# c4 history-less scan: wider column blocks (2 KiB / 4 KiB row segments per block-epoch)
+PATCHES["c4_cb512"] = [("      return launch_elem_shape<VARIANT, 2, VEC, 2, VEC, false, 256, 256, yk::DP_QTE>(st, A);",
+                        "      return launch_elem_shape<VARIANT, 2, VEC, 2, VEC, false, 256, 512, yk::DP_QTE>(st, A);")]
+PATCHES["c4_cb1024"] = [("      return launch_elem_shape<VARIANT, 2, VEC, 2, VEC, false, 256, 256, yk::DP_QTE>(st, A);",
+                         "      return launch_elem_shape<VARIANT, 2, VEC, 2, VEC, false, 256, 1024, yk::DP_QTE>(st, A);")]
+PATCHES["c4_p3"] = [("      return launch_elem_shape<VARIANT, 2, VEC, 2, VEC, false, 256, 256, yk::DP_QTE>(st, A);",
+                     "      return launch_elem_shape<VARIANT, 2, VEC, 3, VEC, false, 256, 256, yk::DP_QTE>(st, A);")]
+PATCHES["c4_p4"] = [("constexpr int kNoHistP2 = 3;", "constexpr int kNoHistP2 = 4;")]

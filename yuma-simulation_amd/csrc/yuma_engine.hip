@@ -4646,6 +4646,9 @@ int launch_bonds_colnorm(RowCfg rc, hipStream_t st, yk::BondArgs& A, int* ptiles
 // scenarios per block (k_bonds_grp's history).
 constexpr int kWideP = 2;      // epochs in flight of the wide history scan
 constexpr int kWidePCn = 2;    // ... for Yuma / Yuma2 (more work per epoch)
+// epochs in flight of the two-row history-less scan (c4 bonds 1.37-1.39 ->
+// 1.33 ms with 3 against 2, profiles/r05/ab_c4_scan.txt)
+constexpr int kNoHistP2 = 3;
 constexpr int kScanGroup = 4;  // scenarios per block of the shared-input scan
 int bonds_rows(bool vec, bool hist, bool wsh) { return vec && (hist || wsh) ? 2 : 1; }
 template <int VARIANT, int R, bool VEC, int P, bool VECI, bool NT, int BS, int CB, int DPL>
@@ -4684,7 +4687,7 @@ int launch_bonds_elem(hipStream_t st, yk::BondArgs& A) {
     // c2's 512 such blocks 0.99 -> 1.31, so one row per lane there
     const long long blocks_r2 = (long long)A.N * ((A.V + 7) / 8) * ((A.M + 255) / 256);
     if (blocks_r2 >= 4096)
-      return launch_elem_shape<VARIANT, 2, VEC, 2, VEC, false, 256, 256, yk::DP_QTE>(st, A);
+      return launch_elem_shape<VARIANT, 2, VEC, kNoHistP2, VEC, false, 256, 256, yk::DP_QTE>(st, A);
     return launch_elem_shape<VARIANT, 1, VEC, 4, VEC, false, 256, 256, yk::DP_QTE>(st, A);
   }
   if (hist) return launch_elem_shape<VARIANT, 2, VEC, 2, VEC, true, 256, 64, yk::DP_TV>(st, A);
