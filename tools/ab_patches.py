@@ -242,7 +242,7 @@ PATCHES["rank_b16"] = [("  constexpr int B = 8;\n  for (int r0 = L.g; r0 < V; r0
                         "  constexpr int B = 16;\n  for (int r0 = L.g; r0 < V; r0 += 16 * B) {")]
 PATCHES["rank_nt"] = [("      const int rr = min(r0 + 16 * i, V - 1);\n      load4c<VEC>(Ws, rr, V, m, M, w[i]);",
                        "      const int rr = min(r0 + 16 * i, V - 1);\n      load4c<VEC, true>(Ws, rr, V, m, M, w[i]);")]
-PATCHES["rankw_plain"] = [("  if (!full && csb && yk::kRankWide) {", "  if (!full && yk::kRankWide) {")]
+PATCHES["rankw_plain"] = [("  if (!full && (csb || M >= 16384) && yk::kRankWide) {", "  if (!full && yk::kRankWide) {")]
 
 # round 5: sweep scan, W ring refill issued after the epoch's per-scenario
 # incentive loads (vmcnt is in issue order: waiting for the next epoch's
@@ -269,4 +269,4 @@ PATCHES["c4_cb1024"] = [("      return launch_elem_shape<VARIANT, 2, VEC, 2, VEC
                          "      return launch_elem_shape<VARIANT, 2, VEC, 2, VEC, false, 256, 1024, yk::DP_QTE>(st, A);")]
 PATCHES["c4_p3"] = [("      return launch_elem_shape<VARIANT, 2, VEC, 2, VEC, false, 256, 256, yk::DP_QTE>(st, A);",
                      "      return launch_elem_shape<VARIANT, 2, VEC, 3, VEC, false, 256, 256, yk::DP_QTE>(st, A);")]
-PATCHES["c4_p4"] = [("constexpr int kNoHistP2 = 3;", "constexpr int kNoHistP2 = 4;")]
+PATCHES["c4_p4"] = [("constexpr int kNoHistP2 = 3;", "constexpr int kNoHistP2 = 4;")]  # 142 VGPRs: c4 bonds 1.34 -> 1.49

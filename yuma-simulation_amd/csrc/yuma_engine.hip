@@ -2056,9 +2056,10 @@ __global__ __launch_bounds__(256, 1) void k_rank_s(const float* __restrict__ W,
 // 4 waves in order (LDS); tile partials as k_rank_s (the 64 miners of a tile
 // by the wave butterfly). Same outputs and options as k_rank_s. Launched for
 // the ranks that also form Yuma / Yuma2's bond column sums (BCS): there it
-// takes 0.75 ms at c2 against 0.79 for k_rank_s; the plain rank is a tie
-// (0.70-0.72 against 0.70, profiles/r05/ab_rank_wide.txt), so k_rank_s stays.
-constexpr int kRankWide = 1;  // launch the wide form for BCS ranks (0: k_rank_s)
+// takes 0.75 ms at c2 against 0.79 for k_rank_s; and for wide subnets (c4
+// 1.10 against 1.15). c2's plain rank is a tie (0.70-0.72 against 0.70,
+// profiles/r05/ab_rank_wide.txt), so k_rank_s stays there.
+constexpr int kRankWide = 1;  // launch the wide form (0: k_rank_s everywhere)
 template <bool VEC, bool YUMA2 = false, bool BCS = false>
 __global__ __launch_bounds__(256, 1) void k_rank_sw(const float* __restrict__ W,
                                                  const float* __restrict__ rsd,
@@ -4502,7 +4503,10 @@ void launch_rank(RowCfg rc, long long nblocks, hipStream_t st, const float* W, c
                  float* Wc, float* tvc, float* tvn, int wsh, const int* crep = nullptr,
                  float* csb = nullptr, float* csr = nullptr, const yuma_params_t* prm = nullptr) {
   const bool full = Wn != nullptr || Wc != nullptr || tvc != nullptr;
-  if (!full && csb && yk::kRankWide) {  // streaming rank + bond column sums on 256-miner column blocks
+  // the wide form for the ranks that also form bond column sums, and for wide
+  // subnets (c4 rank 1.15 -> 1.10 ms; c2's plain rank is a tie, 0.70 both,
+  // profiles/r05/ab_rank_wide.txt, ab_c4_rank.txt)
+  if (!full && (csb || M >= 16384) && yk::kRankWide) {  // streaming rank on 256-miner column blocks
     const long long nb = nblocks / tiles * ((M + 255) / 256);
     if (yuma2 && csb)
       YK_LAUNCH((yk::k_rank_sw<VEC, true, true>), nb, 256, st, W, rsd, sn, C, N, V, M, slice0, tiles,
