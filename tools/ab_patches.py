@@ -270,3 +270,10 @@ PATCHES["c4_cb1024"] = [("      return launch_elem_shape<VARIANT, 2, VEC, 2, VEC
 PATCHES["c4_p3"] = [("      return launch_elem_shape<VARIANT, 2, VEC, 2, VEC, false, 256, 256, yk::DP_QTE>(st, A);",
                      "      return launch_elem_shape<VARIANT, 2, VEC, 3, VEC, false, 256, 256, yk::DP_QTE>(st, A);")]
 PATCHES["c4_p4"] = [("constexpr int kNoHistP2 = 3;", "constexpr int kNoHistP2 = 4;")]  # 142 VGPRs: c4 bonds 1.34 -> 1.49
+# c2 history scan: 512-thread blocks over 2 rows x 2048 miners (8 KiB row runs per block-epoch):
+# bonds 1.54-1.57 -> 1.63-1.66 ms, rejected (profiles/r05/ab_hist_cb2048.txt)
+PATCHES["hist_cb2048"] = [("                               512, 1024, yk::DP_VQ>(st, A);", "                               512, 2048, yk::DP_VQ>(st, A);")]
+
+# round 5: YumaRust's strip scan with 2 / 4 waves per 16-miner strip block
+# (cn_w2 / cn_w4: launch_cn<VARIANT, 8, 2> / <VARIANT, 4, 4> at 256 validators;
+# bonds 3.50 -> 9.12 / 5.11 ms, rejected, profiles/r05/ab_cn_waves.txt)

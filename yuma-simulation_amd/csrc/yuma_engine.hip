@@ -3080,17 +3080,19 @@ __global__ __launch_bounds__(NT) void k_bonds(BondArgs A) {
 constexpr int kCnStrip = 16;  // miners per column-normalised block
 
 
-// Sum over the 8 waves (in order) of per-wave column partials: wave w's DPP
+// Sum over the NW waves (in order) of per-wave column partials: wave w's DPP
 // row tree result for the 16 strip columns sits in red[w][0..15].
+template <int NW>
 __device__ __forceinline__ void cn_wave_sums(float (&x)[4], float (*red)[kCnStrip], int cq, int rr,
                                              int wave) {
 #pragma unroll
   for (int c = 0; c < 4; ++c) x[c] = wsum16(x[c]);
+  if constexpr (NW == 1) return;  // one wave holds the whole column
   if (rr == 0) *reinterpret_cast<float4*>(&red[wave][cq * 4]) = make_float4(x[0], x[1], x[2], x[3]);
   lds_barrier();
   float4 a = *reinterpret_cast<const float4*>(&red[0][cq * 4]);
 #pragma unroll
-  for (int w = 1; w < 8; ++w) {
+  for (int w = 1; w < NW; ++w) {
     const float4 b = *reinterpret_cast<const float4*>(&red[w][cq * 4]);
     a.x = a.x + b.x;
     a.y = a.y + b.y;
@@ -3103,10 +3105,11 @@ __device__ __forceinline__ void cn_wave_sums(float (&x)[4], float (*red)[kCnStri
   x[3] = a.w;
 }
 
-template <int VARIANT, int R, int P>
-__global__ __launch_bounds__(512, 1) void k_bonds_cn(BondArgs A) {
+template <int VARIANT, int R, int P, int NW = 8>
+__global__ __launch_bounds__(64 * NW, 1) void k_bonds_cn(BondArgs A) {
   constexpr bool RUST = VARIANT == YUMA_VARIANT_RUST, YUMA2 = VARIANT == YUMA_VARIANT_YUMA2;
-  __shared__ __attribute__((aligned(16))) float red[2][8][kCnStrip];
+  constexpr int RS = 16 * NW;  // row stride between a lane's rows
+  __shared__ __attribute__((aligned(16))) float red[2][NW][kCnStrip];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int cq = lane >> 4, rr = lane & 15;
   // Strips 2k and 2k + 1 read the two halves of every 128-byte line of their
@@ -3136,7 +3139,7 @@ __global__ __launch_bounds__(512, 1) void k_bonds_cn(BondArgs A) {
     has_old = src != nullptr;
 #pragma unroll
     for (int i = 0; i < R; ++i) {
-      const int row = row0 + 128 * i;
+      const int row = row0 + RS * i;
       if (has_old && row < V && colok)
         load4<true>(src + n * VM + (long long)row * M, m, M, B[i]);
       else
@@ -3157,7 +3160,7 @@ __global__ __launch_bounds__(512, 1) void k_bonds_cn(BondArgs A) {
         have_wp = true;
 #pragma unroll
         for (int i = 0; i < R; ++i) {
-          const int row = row0 + 128 * i;
+          const int row = row0 + RS * i;
           if (row < V && colok) load4<true>(A.Wprev_init + n * VM + (long long)row * M, m, M, Wp[i]);
         }
       }
@@ -3167,7 +3170,7 @@ __global__ __launch_bounds__(512, 1) void k_bonds_cn(BondArgs A) {
       const long long pw = A.wsh ? (long long)(A.t0 - 1) : ps;
 #pragma unroll
       for (int i = 0; i < R; ++i) {
-        const int row = row0 + 128 * i;
+        const int row = row0 + RS * i;
         if (row < V && colok) {
           float x[4];
           load4<true>(A.W + pw * VM + (long long)row * M, m, M, x);
@@ -3189,7 +3192,7 @@ __global__ __launch_bounds__(512, 1) void k_bonds_cn(BondArgs A) {
     const float* Wt = A.W + (A.wsh ? (long long)t : slice) * VM;
 #pragma unroll
     for (int i = 0; i < R; ++i) {
-      const int rr_ = min(row0 + 128 * i, V - 1);
+      const int rr_ = min(row0 + RS * i, V - 1);
       const float4 x = *reinterpret_cast<const float4*>(Wt + (long long)rr_ * M + mc);
       rw[k][i][0] = x.x;
       rw[k][i][1] = x.y;
@@ -3239,7 +3242,7 @@ __global__ __launch_bounds__(512, 1) void k_bonds_cn(BondArgs A) {
       }
 #pragma unroll
       for (int i = 0; i < R; ++i) {
-        const bool live = row0 + 128 * i < V;
+        const bool live = row0 + RS * i < V;
         s[i] = live ? rsn[k][i] : 0.0f;
 #pragma unroll
         for (int c = 0; c < 4; ++c) wn[i][c] = (live && colok) ? wn[i][c] : 0.0f;
@@ -3273,7 +3276,7 @@ __global__ __launch_bounds__(512, 1) void k_bonds_cn(BondArgs A) {
       }
       if (t + P < A.t1) fetch(k, t + P);  // slot k consumed: refill it
       if constexpr (!RUST) {
-        cn_wave_sums(csum, red[par], cq, rr, wave);
+        cn_wave_sums<NW>(csum, red[par], cq, rr, wave);
         par ^= 1;
       }
       float ema[4] = {0.0f, 0.0f, 0.0f, 0.0f};
@@ -3295,7 +3298,7 @@ __global__ __launch_bounds__(512, 1) void k_bonds_cn(BondArgs A) {
         }
 #pragma unroll
         for (int i = 0; i < R; ++i) {
-          const bool live = row0 + 128 * i < V;
+          const bool live = row0 + RS * i < V;
 #pragma unroll
           for (int c = 0; c < 4; ++c) {
             const float b = nan_to_num(bi[i][c], 0.0f);
@@ -3307,7 +3310,7 @@ __global__ __launch_bounds__(512, 1) void k_bonds_cn(BondArgs A) {
         }
       }
       if constexpr (RUST) {  // B_ema / (Σ_v B_ema + 1e-6), nan_to_num (yumas.py:147-149)
-        cn_wave_sums(ema, red[par], cq, rr, wave);
+        cn_wave_sums<NW>(ema, red[par], cq, rr, wave);
         par ^= 1;
         RowDiv cd[4];
 #pragma unroll
@@ -3334,7 +3337,7 @@ __global__ __launch_bounds__(512, 1) void k_bonds_cn(BondArgs A) {
       // column quads of a row: lanes l, l^16, l^32, l^48)
 #pragma unroll
       for (int i = 0; i < R; ++i) {
-        const int row = row0 + 128 * i;
+        const int row = row0 + RS * i;
         if (A.B_hist != nullptr && row < V && colok)
           __builtin_nontemporal_store(fvec4{B[i][0], B[i][1], B[i][2], B[i][3]},
                                       reinterpret_cast<fvec4*>(A.B_hist + slice * VM + (long long)row * M + m));
@@ -3349,7 +3352,7 @@ __global__ __launch_bounds__(512, 1) void k_bonds_cn(BondArgs A) {
   }
 #pragma unroll
   for (int i = 0; i < R; ++i) {
-    const int row = row0 + 128 * i;
+    const int row = row0 + RS * i;
     if (row < V && colok) store4<true>(A.Bstate + n * VM + (long long)row * M, m, M, B[i]);
   }
 }
@@ -4586,14 +4589,26 @@ void launch_rank(RowCfg rc, long long nblocks, hipStream_t st, const float* W, c
 // small subnets and the full-output epoch (W_b / instantaneous bonds stored)
 // k_bonds on 64-miner tiles. Returns the dividend-partial layout and sets
 // *ptiles to the partials per (slice, validator).
-template <int VARIANT, int R>
+template <int VARIANT, int R, int NW = 8>
 int launch_cn(hipStream_t st, yk::BondArgs& A, int* ptiles) {
   A.rowblocks = 1;
   A.cblocks = (A.M + yk::kCnStrip - 1) / yk::kCnStrip;
   *ptiles = A.cblocks;
   const long long nblocks = (long long)A.N * A.cblocks;
-  YK_LAUNCH((yk::k_bonds_cn<VARIANT, R, R <= 2 ? 4 : (R == 4 ? 2 : 1)>), nblocks, 512, st, A);
+  constexpr int P = NW == 8 ? (R <= 2 ? 4 : (R == 4 ? 2 : 1)) : (R <= 4 ? 3 : 2);
+  YK_LAUNCH((yk::k_bonds_cn<VARIANT, R, P, NW>), nblocks, 64 * NW, st, A);
   return yk::DP_TV;
+}
+// YumaRust's strip scan: 8 waves per 16-miner strip. Fewer waves with more
+// rows per lane (a cheaper per-epoch column reduction) lose: c2 YumaRust
+// bonds 3.50 -> 5.11 ms with 4 waves, 9.12 with 2 (profiles/r05/ab_cn_waves.txt)
+template <int VARIANT>
+int launch_cn_rows(hipStream_t st, yk::BondArgs& A, int* ptiles) {
+  const int V = A.V;
+  if (V <= 128) return launch_cn<VARIANT, 1>(st, A, ptiles);
+  if (V <= 256) return launch_cn<VARIANT, 2>(st, A, ptiles);
+  if (V <= 512) return launch_cn<VARIANT, 4>(st, A, ptiles);
+  return launch_cn<VARIANT, 8>(st, A, ptiles);
 }
 template <int VARIANT, bool VEC>
 int launch_bonds_elem(hipStream_t st, yk::BondArgs& A);
@@ -4607,12 +4622,7 @@ int launch_bonds_colnorm(RowCfg rc, hipStream_t st, yk::BondArgs& A, int* ptiles
     }
   }
   if constexpr (VEC) {
-    if (A.V > 64 && A.Wb_out == nullptr && A.Binst_out == nullptr) {
-      if (A.V <= 128) return launch_cn<VARIANT, 1>(st, A, ptiles);
-      if (A.V <= 256) return launch_cn<VARIANT, 2>(st, A, ptiles);
-      if (A.V <= 512) return launch_cn<VARIANT, 4>(st, A, ptiles);
-      return launch_cn<VARIANT, 8>(st, A, ptiles);
-    }
+    if (A.V > 64 && A.Wb_out == nullptr && A.Binst_out == nullptr) return launch_cn_rows<VARIANT>(st, A, ptiles);
   }
   *ptiles = A.tiles;
   A.rowblocks = 1;
