@@ -131,8 +131,13 @@ enum {
   YUMA_EUNSUPPORTED = -4
 };
 
-/* Largest validator count a slice may have (register-resident columns). */
-#define YUMA_MAX_VALIDATORS 1024
+/* Validators per slice. Up to YUMA_REG_VALIDATORS a workgroup holds a miner
+ * column's validators in registers (the fast paths); above, the engine streams
+ * the column from memory in every consensus pass and runs YumaRust's bond
+ * normalisation as two launches per epoch (correct at any size up to
+ * YUMA_MAX_VALIDATORS, built for the occasional very wide validator set). */
+#define YUMA_REG_VALIDATORS 1024
+#define YUMA_MAX_VALIDATORS (1 << 20)
 
 /* Bytes of device workspace yuma_run / yuma_epoch need for these sizes.
  * full_outputs != 0 reserves the partial sums the validator_trust output

@@ -405,9 +405,10 @@ def test_ragged_shapes_vs_oracle(V, M):
 
 
 def test_rejects_too_many_validators():
+    big = 2**20 + 1
     with pytest.raises(engine.EngineError):
         engine.run(engine.VARIANT_YUMA3, [engine.make_params(3, Y.YumaConfig())],
-                   torch.zeros(1, 1, 1025, 8), torch.ones(1, 1, 1025))
+                   torch.zeros(1, 1, big, 1), torch.ones(1, 1, big))
 
 
 def test_deterministic_repeat():

@@ -52,13 +52,16 @@ def test_compute_without_gpu_fails_loudly():
 
 
 def test_engine_limits_raise_clear_errors():
-    """the engine's limits (V <= 1024, consensus_precision
-    <= 2**30; the reference has neither) surface as EngineError with the
-    limit named, before any GPU work (DESIGN.md §3 'Limits')."""
-    with pytest.raises(engine.EngineError, match="1024"):
-        Y.Yuma3(torch.rand(1025, 8), torch.rand(1025))
-    with pytest.raises(engine.EngineError, match="1024"):
-        engine.run(engine.VARIANT_YUMA4, [], torch.zeros(1, 1, 2048, 4), torch.zeros(1, 1, 2048))
+    """the engine's limits (consensus_precision <= 2**30,
+    V <= 2**20 validators; the reference has neither) surface as EngineError
+    with the limit named, before any GPU work (DESIGN.md §3 'Limits'). Above
+    1024 validators the engine streams each miner column (round 5): such a
+    subnet is no longer refused."""
+    big = 2**20 + 1
+    with pytest.raises(engine.EngineError, match=str(2**20)):
+        engine.run(engine.VARIANT_YUMA4, [], torch.zeros(1, 1, big, 1), torch.zeros(1, 1, big))
+    engine.check_limits(1025, 8)  # within the limits now
+    engine.check_limits(2**20, 8)
     cfg = Y.YumaConfig(simulation=Y.SimulationHyperparameters(consensus_precision=2**31))
     with pytest.raises(engine.EngineError, match="2\\*\\*30"):
         Y.Yuma(torch.rand(4, 8), torch.rand(4), config=cfg)

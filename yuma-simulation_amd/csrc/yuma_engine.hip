@@ -53,6 +53,9 @@
 namespace yk {
 
 constexpr int kTileM = 64;
+// validators whose column a workgroup holds in registers / stages in LDS;
+// above, the streaming paths (k_consensus_big, k_rank_sw<BIGV>, ...)
+constexpr int kRegRows = YUMA_REG_VALIDATORS;
 typedef float fvec4 __attribute__((ext_vector_type(4)));       // miner columns per tile: 16 lanes x float4
 constexpr int kMaxTiles = 1 << 20;
 
@@ -730,6 +733,145 @@ __global__ __launch_bounds__(NT) void k_consensus(const float* __restrict__ W,
 #pragma unroll
     for (int c = 0; c < 4; ++c)
       if (m + c < M) craw[slice * M + m + c] = hi[c];
+}
+
+// Consensus above YUMA_REG_VALIDATORS validators: the column no longer fits a
+// workgroup's registers, so every pass of the search streams the 64-miner
+// tile's rows from memory (the normalised weights recomputed per pass with
+// IEEE division, as k_consensus). Pass 0: prerank, bracket (k_consensus'
+// rules); then the bisection on the grid k 2^-iters. Order of every sum:
+// thread-sequential rows g + 16 i, the 4 row groups of a wave, waves in order.
+template <bool VEC>
+__global__ __launch_bounds__(256) void k_consensus_big(const float* __restrict__ W,
+                                                      const float* __restrict__ rsd,
+                                                      const float* __restrict__ sn,
+                                                      const yuma_params_t* __restrict__ prm, int N,
+                                                      int V, int M, long long slice0, int tiles,
+                                                      double* __restrict__ craw,
+                                                      float* __restrict__ Pout, int wsh,
+                                                      const int* __restrict__ crep) {
+  constexpr int NW = 4, G = 16;
+  __shared__ float4 red[2][NW * 16];
+  const Lay L = lay();
+  const long long slice = slice0 + blockIdx.x / tiles;
+  const int tile = blockIdx.x % tiles;
+  const int n = (int)(slice % N);
+  if (dup_slice(crep, slice, N)) return;  // block-uniform
+  const int m = tile * kTileM + L.c4 * 4;
+  const float* Ws = W + in_slice(slice, N, wsh) * (long long)V * M;
+  const float* rs = rsd + slice * V;
+  const float* ss = sn + slice * V;
+  // row `row`'s normalised weights of this lane's 4 columns (0 outside) and stake
+  auto row_w = [&](int row, float (&x)[4]) -> float {
+    load4c<VEC>(Ws, row, V, m, M, x);
+    const int rr = row < V ? row : V - 1;
+    const RowDiv rdv = row_div(rs[rr]);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) x[c] = div_rn(x[c], rdv);
+    mask4(row, V, m, M, x);
+    return row < V ? ss[rr] : 0.0f;
+  };
+  const float kappa = prm[n].kappa;
+  const int iters = prm[n].bisect_iters;
+  const int top = 1 << iters;
+  const float scale = (float)top, inv_scale = 1.0f / scale;
+  float pacc[4] = {0.0f, 0.0f, 0.0f, 0.0f}, vmax[4], vmin[4], stot[4];
+  bool odd_stake = false;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    vmax[c] = -INFINITY;
+    vmin[c] = INFINITY;
+    stot[c] = 0.0f;
+  }
+  for (int row = L.g; row < V; row += G) {
+    float x[4];
+    const float s = row_w(row, x);
+    odd_stake |= !(s >= 0.0f) || s == INFINITY;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      pacc[c] = pacc[c] + s * x[c];
+      vmax[c] = x[c] > vmax[c] ? x[c] : vmax[c];  // a NaN weight is never counted
+      const float xm = x[c] == x[c] ? x[c] : 0.0f;
+      vmin[c] = xm < vmin[c] ? xm : vmin[c];
+      stot[c] = stot[c] + s;
+    }
+  }
+  if (Pout != nullptr) {
+    col_reduce4<NW>(pacc, red[1], L);
+    if (L.g == 0)
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        if (m + c < M) Pout[slice * M + m + c] = pacc[c];
+    __syncthreads();
+  }
+  const bool bracket = !__syncthreads_or(odd_stake) && kappa >= 0.0f;
+  int lo_k[4], hi_k[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    lo_k[c] = 0;
+    hi_k[c] = top;
+  }
+  if (bracket) {
+    col_reduce4_max<NW>(vmax, red[0], L);
+    __syncthreads();
+    col_reduce4_min<NW>(vmin, red[1], L);
+    __syncthreads();
+    col_reduce4<NW>(stot, red[0], L);
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int gmax = vmax[c] > 0.0f ? (int)fminf(ceilf(vmax[c] * scale), scale) : 0;
+      const int gmin = vmin[c] > 0.0f ? (int)fminf(ceilf(vmin[c] * scale), scale + 1.0f) : 0;
+      int lo_c = gmin >= 2 ? gmin - 1 : 0;
+      int hi_c = gmax < 1 ? 1 : gmax;
+      if (lo_c > 0 && !(stot[c] > kappa)) {
+        lo_c = 0;
+        hi_c = 1;
+      }
+      if (lo_c >= top) {
+        lo_c = top - 1;
+        hi_c = top;
+      }
+      if (hi_c <= lo_c) hi_c = lo_c + 1;
+      lo_k[c] = lo_c;
+      hi_k[c] = hi_c;
+    }
+  }
+  for (int it = 0;; ++it) {
+    bool active = false;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) active |= (hi_k[c] - lo_k[c]) > 1;
+    if (!__syncthreads_or(active)) break;
+    float part[4], midf[4];
+    int mid[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      mid[c] = (lo_k[c] + hi_k[c]) >> 1;
+      midf[c] = (float)mid[c] * inv_scale;
+      part[c] = 0.0f;
+    }
+    for (int row = L.g; row < V; row += G) {
+      float x[4];
+      const float s = row_w(row, x);
+      const float zs = 0.0f * s;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) part[c] = part[c] + ((x[c] > midf[c]) ? s : zs);
+    }
+    col_reduce4<NW>(part, red[it & 1], L);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      if (hi_k[c] - lo_k[c] > 1) {
+        if (part[c] > kappa)
+          lo_k[c] = mid[c];
+        else
+          hi_k[c] = mid[c];
+      }
+    }
+  }
+  if (L.g == 0)
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      if (m + c < M) craw[slice * M + m + c] = (double)hi_k[c] / (double)top;
 }
 
 // ---------------------------------------------------------------------------
@@ -1931,7 +2073,7 @@ __global__ __launch_bounds__(256, 1) void k_rank_s(const float* __restrict__ W,
   // the slice's row sums, their IEEE reciprocals and the stakes staged in LDS
   // once per block (coalesced), instead of two per-lane scalar loads per row
   // and a reciprocal per row in every lane
-  __shared__ float rows_d[YUMA_MAX_VALIDATORS], rows_r[YUMA_MAX_VALIDATORS], rows_s[YUMA_MAX_VALIDATORS];
+  __shared__ float rows_d[kRegRows], rows_r[kRegRows], rows_s[kRegRows];
   for (int j = threadIdx.x; j < V; j += 256) {
     const float dj = rsd[wsl * V + j];
     rows_d[j] = dj;
@@ -2059,8 +2201,10 @@ __global__ __launch_bounds__(256, 1) void k_rank_s(const float* __restrict__ W,
 // takes 0.75 ms at c2 against 0.79 for k_rank_s; and for wide subnets (c4
 // 1.10 against 1.15). c2's plain rank is a tie (0.70-0.72 against 0.70,
 // profiles/r05/ab_rank_wide.txt), so k_rank_s stays there.
+// BIGV (above kRegRows validators): the row sums, reciprocals and stakes are
+// read per row from memory instead of the LDS staging.
 constexpr int kRankWide = 1;  // launch the wide form (0: k_rank_s everywhere)
-template <bool VEC, bool YUMA2 = false, bool BCS = false>
+template <bool VEC, bool YUMA2 = false, bool BCS = false, bool BIGV = false>
 __global__ __launch_bounds__(256, 1) void k_rank_sw(const float* __restrict__ W,
                                                  const float* __restrict__ rsd,
                                                  const float* __restrict__ sn,
@@ -2104,34 +2248,42 @@ __global__ __launch_bounds__(256, 1) void k_rank_sw(const float* __restrict__ W,
   }
   float Cc[4];
   load4c<VEC>(C + slice * M, 0, 1, m, M, Cc);
-  __shared__ float rows_d[YUMA_MAX_VALIDATORS], rows_r[YUMA_MAX_VALIDATORS], rows_s[YUMA_MAX_VALIDATORS];
-  for (int j = threadIdx.x; j < V; j += 256) {
-    const float dj = rsd[wsl * V + j];
-    rows_d[j] = dj;
-    rows_r[j] = 1.0f / dj;
-    rows_s[j] = sn[slice * V + j];
+  __shared__ float rows_d[BIGV ? 1 : kRegRows], rows_r[BIGV ? 1 : kRegRows], rows_s[BIGV ? 1 : kRegRows];
+  if constexpr (!BIGV) {
+    for (int j = threadIdx.x; j < V; j += 256) {
+      const float dj = rsd[wsl * V + j];
+      rows_d[j] = dj;
+      rows_r[j] = 1.0f / dj;
+      rows_s[j] = sn[slice * V + j];
+    }
+    __syncthreads();
   }
-  __syncthreads();
   float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
   float acb[4] = {0.0f, 0.0f, 0.0f, 0.0f};
   unsigned ymx[4] = {0u, 0u, 0u, 0u}, ymn[4] = {~0u, ~0u, ~0u, ~0u};
   constexpr int B = 8;
   for (int r0 = wave; r0 < V; r0 += 4 * B) {
-    float w[B][4], d[B], s[B];
+    float w[B][4], d[B], s[B], rcp[B];
 #pragma unroll
     for (int i = 0; i < B; ++i) {
       const int rr = min(r0 + 4 * i, V - 1);
       load4c<VEC>(Ws, rr, V, m, M, w[i]);
-      d[i] = rows_d[rr];
-      s[i] = rows_s[rr];
+      if constexpr (BIGV) {
+        d[i] = rsd[wsl * V + rr];
+        s[i] = sn[slice * V + rr];
+        rcp[i] = 1.0f / d[i];
+      } else {
+        d[i] = rows_d[rr];
+        s[i] = rows_s[rr];
+        rcp[i] = rows_r[rr];
+      }
     }
     if (!YUMA2 || divide) {
       bool slow = false;
 #pragma unroll
       for (int i = 0; i < B; ++i) {
-        const int rr = min(r0 + 4 * i, V - 1);
         const float ad = fabsf(d[i]);
-        const RowDiv rdv{d[i], rows_r[rr], ad >= 0x1p-60f && ad <= 0x1p60f};
+        const RowDiv rdv{d[i], rcp[i], ad >= 0x1p-60f && ad <= 0x1p60f};
 #pragma unroll
         for (int c = 0; c < 4; ++c) w[i][c] = div_fast_nz(w[i][c], rdv, slow);
       }
@@ -2196,6 +2348,85 @@ __global__ __launch_bounds__(256, 1) void k_rank_sw(const float* __restrict__ W,
     if (mg < M) {
       csb[slice * M + mg] = b;
       csr[slice * M + mg] = ok ? 1.0f / b : qnan();
+    }
+  }
+}
+
+// The full outputs of the clip above kRegRows validators (the register-
+// resident k_rank_w / k_rank form them at or below): the normalised weights
+// Wn (yumas.py:186), the clipped weights Wc = min(src, C) (:214; Yuma2 clips
+// W_prev, :328) and the per-tile row sums of Wc and Wn that validator_trust
+// T_v = sum Wc / sum Wn divides (:224; k_finalize adds the tiles in order).
+// Block = one 64-miner tile of a slice, rows g + 16 i per thread; every
+// division IEEE-exact (div_rn).
+template <bool VEC, bool YUMA2>
+__global__ __launch_bounds__(256) void k_full_big(const float* __restrict__ W,
+                                                 const float* __restrict__ rsd,
+                                                 const float* __restrict__ C, int N, int V, int M,
+                                                 long long slice0, int tiles, int wsh,
+                                                 const float* __restrict__ Wprev_init,
+                                                 float* __restrict__ Wn_out, float* __restrict__ Wc_out,
+                                                 float* __restrict__ tvc, float* __restrict__ tvn) {
+  const Lay L = lay();
+  const long long slice = slice0 + blockIdx.x / tiles;
+  const int tile = blockIdx.x % tiles;
+  const int m = tile * kTileM + L.c4 * 4;
+  const long long VM = (long long)V * M;
+  const float* Ws = W + in_slice(slice, N, wsh) * VM;
+  // Yuma2's clipped source: the previous slice's normalised weights (the
+  // caller's W_prev at the first epoch, or W itself without one)
+  const float* Wp = Ws;
+  long long psl = slice;
+  bool pdiv = true;
+  if (YUMA2) {
+    if (slice >= N) {
+      psl = slice - N;
+      Wp = W + in_slice(psl, N, wsh) * VM;
+    } else if (Wprev_init != nullptr) {
+      Wp = Wprev_init + (slice % N) * VM;
+      pdiv = false;
+    }
+  }
+  float Cc[4];
+  load4c<VEC>(C + slice * M, 0, 1, m, M, Cc);
+  for (int row = L.g; row < V; row += 16) {
+    float x[4], src[4];
+    load4c<VEC>(Ws, row, V, m, M, x);
+    const RowDiv rdv = row_div(rsd[slice * V + min(row, V - 1)]);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) x[c] = div_rn(x[c], rdv);
+    if (YUMA2) {
+      load4c<VEC>(Wp, row, V, m, M, src);
+      if (pdiv) {
+        const RowDiv pdv = row_div(rsd[psl * V + min(row, V - 1)]);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) src[c] = div_rn(src[c], pdv);
+      }
+    } else {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) src[c] = x[c];
+    }
+    float wc[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) wc[c] = tmin(src[c], Cc[c]);
+    if (row < V) {
+      if (Wn_out != nullptr) store4<VEC>(Wn_out + slice * VM + (long long)row * M, m, M, x);
+      if (Wc_out != nullptr) store4<VEC>(Wc_out + slice * VM + (long long)row * M, m, M, wc);
+    }
+    if (tvc != nullptr) {
+      float a = 0.0f, b = 0.0f;
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        if (m + c < M) {
+          a = a + wc[c];
+          b = b + x[c];
+        }
+      a = sum_row16(a);
+      b = sum_row16(b);
+      if (L.c4 == 0 && row < V) {
+        tvc[(slice * tiles + tile) * (long long)V + row] = a;
+        tvn[(slice * tiles + tile) * (long long)V + row] = b;
+      }
     }
   }
 }
@@ -2752,6 +2983,7 @@ struct BondArgs {
   const float* csb;   // Yuma / Yuma2: [slice][M] Σ_v S·W_b (k_rank_s), or null
   const float* csr;   // ... RN(1 / csb) or NaN (the column fails the division screen)
   const float* R;     // [slice][M] rank R = Σ_v S·Wc (YumaRust's first bond column sum)
+  float* cpart;       // YumaRust above kRegRows validators: [N][row block][M] column partials
   int N, V, M, tiles, rowblocks, t0, t1;
   int wsh;      // every scenario reads input slice t (yuma_run_shared)
   int cblocks;  // k_bonds_elem: column blocks of CB miners per row block
@@ -3358,6 +3590,123 @@ __global__ __launch_bounds__(64 * NW, 1) void k_bonds_cn(BondArgs A) {
 }
 
 // ---------------------------------------------------------------------------
+// YumaRust above kRegRows validators: the bond column normalisation of an
+// epoch (yumas.py:147-149) needs the column sums over every validator, which
+// no workgroup holds, so each epoch is two launches over (scenario, 64-row
+// block, 64-miner tile) blocks:
+//   k_rust_big_ema   B = nan_to_num(S·Wc / (R + 1e-6)) (:113-116; the
+//                    column sum B_sum is R's expression, :103), the EMA
+//                    α·B + (1-α)·B_old or B (:142-145) into the bond state,
+//                    and the block's column partial sums of it;
+//   k_rust_big_norm  Z = the partials in row-block order + 1e-6, B_ema / Z
+//                    with nan_to_num, the bond history, and the per-tile
+//                    dividend partials Σ B·I ([slice][tile][V], k_finalize).
+// ---------------------------------------------------------------------------
+constexpr int kRustBigRows = 64;  // rows per block: 16 row groups x 4
+template <bool VEC>
+__global__ __launch_bounds__(256) void k_rust_big_ema(BondArgs A, int t, float* __restrict__ cpart) {
+  __shared__ float4 red[4 * 16];
+  const Lay L = lay();
+  const int tile = blockIdx.x % A.tiles;
+  const int rb = (blockIdx.x / A.tiles) % A.rowblocks;
+  const int n = blockIdx.x / (A.tiles * A.rowblocks);
+  const int N = A.N, V = A.V, M = A.M;
+  const long long VM = (long long)V * M;
+  const long long slice = (long long)t * N + n;
+  const int m = tile * kTileM + L.c4 * 4;
+  const yuma_params_t& pg = A.prm[n];
+  const bool liquid = pg.liquid_mode != YUMA_LIQUID_OFF;
+  // the bond state before this epoch: the caller's B_init (or none) at epoch 0
+  const float* Bsrc = (t == 0) ? A.B_init : A.Bstate;
+  const bool has_old = Bsrc != nullptr;
+  float Cc[4], Rc[4], bac[4], omba[4];
+  load4c<VEC>(A.C + slice * M, 0, 1, m, M, Cc);
+  load4c<VEC>(A.R + slice * M, 0, 1, m, M, Rc);
+  if (liquid) {
+    load4c<VEC>(A.ba + slice * M, 0, 1, m, M, bac);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) omba[c] = 1.0f - bac[c];
+  } else {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      bac[c] = pg.bond_alpha;
+      omba[c] = pg.one_minus_bond_alpha;
+    }
+  }
+  const float* Wt = A.W + (A.wsh ? (long long)t : slice) * VM;
+  float csum[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+  for (int i = 0; i < kRustBigRows / 16; ++i) {
+    const int row = rb * kRustBigRows + L.g + 16 * i;
+    float x[4], e[4];
+    load4c<VEC>(Wt, row, V, m, M, x);
+    const int rr = row < V ? row : V - 1;
+    const RowDiv rdv = row_div(A.rsd[slice * V + rr]);
+    const float sv = A.sn[slice * V + rr];
+    float bo[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    if (has_old && row < V) load4<VEC>(Bsrc + n * VM + (long long)row * M, m, M, bo);
+    float bi[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const float wn = div_rn(x[c], rdv);
+      const float wc = tmin(wn, Cc[c]);
+      bi[c] = nan_to_num((sv * wc) / (Rc[c] + 1e-6f), 0.0f);
+      e[c] = has_old ? bac[c] * bi[c] + omba[c] * bo[c] : bi[c];
+      e[c] = (row < V && m + c < M) ? e[c] : 0.0f;
+      csum[c] = csum[c] + e[c];
+    }
+    if (row < V) {
+      if (A.Binst_out != nullptr) store4<VEC>(A.Binst_out + slice * VM + (long long)row * M, m, M, bi);
+      store4<VEC>(A.Bstate + n * VM + (long long)row * M, m, M, e);
+    }
+  }
+  col_reduce4<4>(csum, red, L);
+  if (L.g == 0)
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      if (m + c < M) cpart[((long long)n * A.rowblocks + rb) * M + m + c] = csum[c];
+}
+
+template <bool VEC>
+__global__ __launch_bounds__(256) void k_rust_big_norm(BondArgs A, int t, const float* __restrict__ cpart) {
+  const Lay L = lay();
+  const int tile = blockIdx.x % A.tiles;
+  const int rb = (blockIdx.x / A.tiles) % A.rowblocks;
+  const int n = blockIdx.x / (A.tiles * A.rowblocks);
+  const int N = A.N, V = A.V, M = A.M;
+  const long long VM = (long long)V * M;
+  const long long slice = (long long)t * N + n;
+  const int m = tile * kTileM + L.c4 * 4;
+  float Z[4], Ic[4];
+  load4c<VEC>(A.I + slice * M, 0, 1, m, M, Ic);
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const int mc = min(m + c, M - 1);
+    float z = 0.0f;
+    for (int b = 0; b < A.rowblocks; ++b) z = z + cpart[((long long)n * A.rowblocks + b) * M + mc];
+    Z[c] = z + 1e-6f;
+  }
+#pragma unroll
+  for (int i = 0; i < kRustBigRows / 16; ++i) {
+    const int row = rb * kRustBigRows + L.g + 16 * i;
+    float e[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    if (row < V) load4<VEC>(A.Bstate + n * VM + (long long)row * M, m, M, e);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) e[c] = nan_to_num(e[c] / Z[c], 0.0f);
+    if (row < V) {
+      store4<VEC>(A.Bstate + n * VM + (long long)row * M, m, M, e);
+      if (A.B_hist != nullptr) store4<VEC>(A.B_hist + slice * VM + (long long)row * M, m, M, e);
+    }
+    float d = 0.0f;
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      if (m + c < M) d = d + e[c] * Ic[c];
+    d = sum_row16(d);
+    if (L.c4 == 0 && row < V) A.dpart[dp_index(slice, tile, row, A.tiles, V)] = d;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Phase 2, element-wise variants (Yuma3 yumas.py:452-472, Yuma4 :570-586):
 // a software-pipelined scan. Each thread owns R rows x 4 miners of the bond
 // tile in registers and keeps the inputs of the next P epochs in flight
@@ -3573,13 +3922,13 @@ __global__ __launch_bounds__(BS, 1) void k_bonds_elem(BondArgs A) {
           // α·B + (1-α)·B_old, or B itself without a bond state (:255-258)
           // (min: C is a quantised level >= +0, so v_minimum's -0 < +0 order
           // gives torch.min's bits)
-          float num[4], b[4];
+          float num[4], b[4], wbv[4];
 #pragma unroll
           for (int c = 0; c < 4; ++c) {
             const float src = (YUMA2 && have_wp) ? Wp[i][c] : wn[c];
             const float wc = vmin(src, rcc[k][c]);
-            const float wb = p_ompen * src + p_pen * wc;
-            num[c] = rsn[k][i] * wb;
+            wbv[c] = p_ompen * src + p_pen * wc;
+            num[c] = rsn[k][i] * wbv[c];
           }
           if (cfast) {
             // RN(num / csb) from RN(1 / csb) (RowDiv's correction; the screen
@@ -3594,6 +3943,9 @@ __global__ __launch_bounds__(BS, 1) void k_bonds_elem(BondArgs A) {
 #pragma unroll
             for (int c = 0; c < 4; ++c) b[c] = nan_to_num(num[c] / rcs[k][c], 0.0f);
           }
+          // the full outputs weight_for_bond / validator_bond (yumas.py:274-275)
+          if (A.Wb_out != nullptr && row < V) store4<VEC>(A.Wb_out + slice * VM + (long long)row * M, m, M, wbv);
+          if (A.Binst_out != nullptr && row < V) store4<VEC>(A.Binst_out + slice * VM + (long long)row * M, m, M, b);
 #pragma unroll
           for (int c = 0; c < 4; ++c) {
             B[i][c] = has_old ? bac[c] * b[c] + omba[c] * B[i][c] : b[c];
@@ -4062,7 +4414,7 @@ __global__ __launch_bounds__(256) void k_finalize(const float* __restrict__ dpar
   // canonical order (dp_quad): per-group sequential, then groups 0..3.
   __shared__ float part[4][256];
   __shared__ float red[4];
-  __shared__ float dsh[YUMA_MAX_VALIDATORS];
+  __shared__ float dsh[kRegRows];
   const long long slice = slice0 + blockIdx.x;
   const int tg = threadIdx.x >> 6, vq = threadIdx.x & 63;
   const int nq = dp_quads(tiles);
@@ -4159,6 +4511,61 @@ __global__ __launch_bounds__(256) void k_finalize(const float* __restrict__ dpar
       for (int k = 0; k < ttiles; ++k) {
         a = a + tvc[(slice * ttiles + k) * V + v];
         b = b + tvn[(slice * ttiles + k) * V + v];
+      }
+      Tv[slice * V + v] = a / b;
+    }
+  }
+}
+
+// k_finalize above kRegRows validators (no LDS copy of D): one thread per
+// validator forms D[v] in the canonical order of the same layouts, parks it in
+// dtmp, and a second pass divides by the block's total (the same
+// thread-sequential + block_sum order as k_finalize).
+__global__ __launch_bounds__(256) void k_finalize_big(const float* __restrict__ dpart,
+                                                      const float* __restrict__ sn, int variant,
+                                                      int V, long long slice0, int tiles,
+                                                      const float* __restrict__ tvc,
+                                                      const float* __restrict__ tvn,
+                                                      float* __restrict__ Dn, float* __restrict__ D,
+                                                      float* __restrict__ Tv, int dpl, int ttiles,
+                                                      float* __restrict__ dtmp) {
+  __shared__ float red[4];
+  const long long slice = slice0 + blockIdx.x;
+  const int nq = dp_quads(tiles);
+  float local = 0.0f;
+  for (int v = threadIdx.x; v < V; v += 256) {
+    float d;
+    if (dpl == DP_PRE) {
+      d = dpart[slice * V + v];
+    } else {
+      float pg[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+      if (dpl == DP_VQ) {
+        const float* pv = dpart + (slice * V + v) * (long long)nq;
+        for (int b = 0; b < nq; ++b) pg[b & 3] = pg[b & 3] + pv[b];
+      } else {
+        const float* dp = dpart + slice * (long long)tiles * V + v;
+        for (int b = 0; b < nq; ++b) pg[b & 3] = pg[b & 3] + dp_quad(dp, V, b, tiles);
+      }
+      d = pg[0];
+      d = d + pg[1];
+      d = d + pg[2];
+      d = d + pg[3];
+    }
+    if (variant == YUMA_VARIANT_YUMA4) d = sn[slice * V + v] * d;
+    dtmp[slice * V + v] = d;
+    local = local + d;
+  }
+  const float tot = block_sum<256>(local, red);
+  const float den = tot + 1e-6f;
+  for (int v = threadIdx.x; v < V; v += 256) {
+    const float d = dtmp[slice * V + v];
+    if (Dn != nullptr) Dn[slice * V + v] = d / den;
+    if (D != nullptr) D[slice * V + v] = d;
+    if (Tv != nullptr) {
+      float a = 0.0f, b = 0.0f;
+      for (int k = 0; k < ttiles; ++k) {
+        a = a + tvc[(slice * ttiles + k) * (long long)V + v];
+        b = b + tvn[(slice * ttiles + k) * (long long)V + v];
       }
       Tv[slice * V + v] = a / b;
     }
@@ -4355,6 +4762,7 @@ struct Workspace {
   int* rcrep;  // per scenario: rank class representative (Yuma: + bond_penalty)
   float* csb;  // Yuma / Yuma2: [slice][M] Σ_v S·W_b (k_rank_s)
   float* csr;  // ... and RN(1 / csb) where the column passes the division screen, else NaN
+  float* cpart;  // YumaRust above kRegRows validators: [N][row block][M]
   size_t bytes;
 };
 
@@ -4403,6 +4811,9 @@ Workspace carve(char* base, int variant, int N, int E, int V, int M, int full) {
   const bool cn = variant == YUMA_VARIANT_YUMA1 || variant == YUMA_VARIANT_YUMA2;
   w.csb = cn ? (float*)take(S * M * 4) : nullptr;
   w.csr = cn ? (float*)take(S * M * 4) : nullptr;
+  w.cpart = (variant == YUMA_VARIANT_RUST && V > yk::kRegRows)
+                ? (float*)take((size_t)N * ((V + yk::kRustBigRows - 1) / yk::kRustBigRows) * M * 4)
+                : nullptr;
   w.bytes = off;
   return w;
 }
@@ -4445,6 +4856,11 @@ void launch_consensus(RowCfg rc, long long nblocks, hipStream_t st, const float*
                       const yuma_params_t* prm, int N, int V, int M, long long slice0, int tiles,
                       double* craw, float* P, int wsh, const int* crep,
                       const float4* rq4 = nullptr) {
+  if (V > yk::kRegRows) {  // the column streamed per search pass
+    YK_LAUNCH(yk::k_consensus_big<VEC>, nblocks, 256, st, W, rsd, sn, prm, N, V, M, slice0, tiles, craw, P,
+              wsh, crep);
+    return;
+  }
   switch (rc) {  // wave-owned columns up to 256 validators
     case RC_256_1:
       launch_consensus_w<1, VEC>(nblocks, st, W, rsd, sn, sx, prm, N, V, M, slice0, tiles, craw,
@@ -4506,6 +4922,30 @@ void launch_rank(RowCfg rc, long long nblocks, hipStream_t st, const float* W, c
                  float* Wc, float* tvc, float* tvn, int wsh, const int* crep = nullptr,
                  float* csb = nullptr, float* csr = nullptr, const yuma_params_t* prm = nullptr) {
   const bool full = Wn != nullptr || Wc != nullptr || tvc != nullptr;
+  if (V > yk::kRegRows) {  // streamed rows: the wide rank with per-row loads, plus the full outputs
+    const long long nb = nblocks / tiles * ((M + 255) / 256);
+    if (yuma2 && csb)
+      YK_LAUNCH((yk::k_rank_sw<VEC, true, true, true>), nb, 256, st, W, rsd, sn, C, N, V, M, slice0, tiles,
+                R, rpart, wsh, nullptr, Wprev_init, csb, csr, prm);
+    else if (yuma2)
+      YK_LAUNCH((yk::k_rank_sw<VEC, true, false, true>), nb, 256, st, W, rsd, sn, C, N, V, M, slice0, tiles,
+                R, rpart, wsh, nullptr, Wprev_init, nullptr, nullptr, prm);
+    else if (csb)
+      YK_LAUNCH((yk::k_rank_sw<VEC, false, true, true>), nb, 256, st, W, rsd, sn, C, N, V, M, slice0, tiles,
+                R, rpart, wsh, full ? nullptr : crep, nullptr, csb, csr, prm);
+    else
+      YK_LAUNCH((yk::k_rank_sw<VEC, false, false, true>), nb, 256, st, W, rsd, sn, C, N, V, M, slice0, tiles,
+                R, rpart, wsh, full ? nullptr : crep, nullptr, nullptr, nullptr, prm);
+    if (full) {
+      if (yuma2)
+        YK_LAUNCH((yk::k_full_big<VEC, true>), nblocks, 256, st, W, rsd, C, N, V, M, slice0, tiles, wsh,
+                  Wprev_init, Wn, Wc, tvc, tvn);
+      else
+        YK_LAUNCH((yk::k_full_big<VEC, false>), nblocks, 256, st, W, rsd, C, N, V, M, slice0, tiles, wsh,
+                  Wprev_init, Wn, Wc, tvc, tvn);
+    }
+    return;
+  }
   // the wide form for the ranks that also form bond column sums, and for wide
   // subnets (c4 rank 1.15 -> 1.10 ms; c2's plain rank is a tie, 0.70 both,
   // profiles/r05/ab_rank_wide.txt, ab_c4_rank.txt)
@@ -4614,6 +5054,21 @@ template <int VARIANT, bool VEC>
 int launch_bonds_elem(hipStream_t st, yk::BondArgs& A);
 template <int VARIANT, bool VEC>
 int launch_bonds_colnorm(RowCfg rc, hipStream_t st, yk::BondArgs& A, int* ptiles) {
+  if (A.V > yk::kRegRows) {  // no workgroup holds a column: streaming forms
+    *ptiles = A.tiles;
+    if constexpr (VARIANT == YUMA_VARIANT_RUST) {
+      A.rowblocks = (A.V + yk::kRustBigRows - 1) / yk::kRustBigRows;
+      A.cblocks = A.tiles;
+      const long long nb = (long long)A.N * A.rowblocks * A.tiles;
+      for (int t = A.t0; t < A.t1; ++t) {
+        YK_LAUNCH((yk::k_rust_big_ema<VEC>), nb, 256, st, A, t, A.cpart);
+        YK_LAUNCH((yk::k_rust_big_norm<VEC>), nb, 256, st, A, t, A.cpart);
+      }
+      return yk::DP_TV;
+    } else {
+      return launch_bonds_elem<VARIANT, VEC>(st, A);  // the rank pass formed csb
+    }
+  }
   if constexpr (VARIANT != YUMA_VARIANT_RUST) {
     // the rank pass formed the bond column sums: element-wise scan
     if (A.csb != nullptr && A.Wb_out == nullptr && A.Binst_out == nullptr) {
@@ -4804,7 +5259,10 @@ int run_impl(int variant, const yuma_params_t* prm, int N, int E, int V, int M, 
   // Yuma / Yuma2 run outputs above 64 validators: the streaming rank also
   // forms the bond column sums Σ_v S·W_b and the bond scan is element-wise
   const bool streaming = out->Wn == nullptr && out->Wc == nullptr && ws.tvc == nullptr;
-  float* csb = (ws.csb != nullptr && streaming && V > 64 && out->Wb == nullptr && out->B_inst == nullptr)
+  // (above kRegRows validators always: the element-wise scan is the only
+  // Yuma / Yuma2 bond scan there, and it writes W_b / B_inst itself)
+  float* csb = (ws.csb != nullptr &&
+                (V > yk::kRegRows || (streaming && V > 64 && out->Wb == nullptr && out->B_inst == nullptr)))
                    ? ws.csb : nullptr;
   const bool rank_stream = streaming && variant != YUMA_VARIANT_YUMA2;  // Yuma2's W_prev: rank per scenario
   const int* rcrep = rank_stream ? crep : nullptr;
@@ -4885,6 +5343,7 @@ int run_impl(int variant, const yuma_params_t* prm, int N, int E, int V, int M, 
     A.csb = csb;
     A.csr = ws.csr;
     A.R = Rr;
+    A.cpart = ws.cpart;
     A.N = N;
     A.V = V;
     A.M = M;
@@ -4905,8 +5364,12 @@ int run_impl(int variant, const yuma_params_t* prm, int N, int E, int V, int M, 
       dsrc = ws.dsum;
       dpl = yk::DP_PRE;
     }
-    YK_LAUNCH(yk::k_finalize, ns, 256, st, dsrc, ws.sn, variant, V, s0, ptiles, ws.tvc,
-              ws.tvn, out->Dn, out->D, out->Tv, dpl, tiles);
+    if (V > yk::kRegRows)
+      YK_LAUNCH(yk::k_finalize_big, ns, 256, st, dsrc, ws.sn, variant, V, s0, ptiles, ws.tvc, ws.tvn, out->Dn,
+                out->D, out->Tv, dpl, tiles, ws.dsum);
+    else
+      YK_LAUNCH(yk::k_finalize, ns, 256, st, dsrc, ws.sn, variant, V, s0, ptiles, ws.tvc,
+                ws.tvn, out->Dn, out->D, out->Tv, dpl, tiles);
     if (out->Sn != nullptr)
       (void)hipMemcpyAsync(out->Sn + s0 * V, ws.sn + s0 * V, (size_t)ns * V * 4,
                            hipMemcpyDeviceToDevice, st);
@@ -4978,8 +5441,9 @@ int shard_stage_impl(int stage, int variant, const yuma_params_t* prm, int N, in
   const long long ns = (long long)E * N;
   // Yuma / Yuma2: the bond column sums are sums over validators, local to
   // the shard's columns: formed by stage 3's rank pass, read by stage 4's scan
-  float* shard_csb = (ws.csb != nullptr && !full && V > 64 && out->Wn == nullptr && out->Wc == nullptr &&
-                      out->Wb == nullptr && out->B_inst == nullptr)
+  float* shard_csb = (ws.csb != nullptr &&
+                      (V > yk::kRegRows || (!full && V > 64 && out->Wn == nullptr && out->Wc == nullptr &&
+                                            out->Wb == nullptr && out->B_inst == nullptr)))
                          ? ws.csb : nullptr;
   switch (stage) {
     case 1: {
@@ -5058,6 +5522,7 @@ int shard_stage_impl(int stage, int variant, const yuma_params_t* prm, int N, in
       A.csb = shard_csb;
       A.csr = ws.csr;
       A.R = R;
+      A.cpart = ws.cpart;
       A.N = N;
       A.V = V;
       A.M = M;
@@ -5078,9 +5543,14 @@ int shard_stage_impl(int stage, int variant, const yuma_params_t* prm, int N, in
     case 5: {
       if (!io->dsum) return fail(YUMA_EINVAL, "stage 5 needs io->dsum");
       if (full && !io->tv) return fail(YUMA_EINVAL, "stage 5 with out->Tv needs io->tv");
-      YK_LAUNCH(yk::k_finalize, ns, 256, st, io->dsum, ws.sn, variant, V, 0LL, 1,
-                full ? io->tv : nullptr, full ? io->tv + ns * V : nullptr, out->Dn, out->D,
-                out->Tv, (int)yk::DP_TV, 1);
+      if (V > yk::kRegRows)
+        YK_LAUNCH(yk::k_finalize_big, ns, 256, st, io->dsum, ws.sn, variant, V, 0LL, 1,
+                  full ? io->tv : nullptr, full ? io->tv + ns * V : nullptr, out->Dn, out->D, out->Tv,
+                  (int)yk::DP_TV, 1, ws.dsum);
+      else
+        YK_LAUNCH(yk::k_finalize, ns, 256, st, io->dsum, ws.sn, variant, V, 0LL, 1,
+                  full ? io->tv : nullptr, full ? io->tv + ns * V : nullptr, out->Dn, out->D,
+                  out->Tv, (int)yk::DP_TV, 1);
       if (out->Sn != nullptr)
         (void)hipMemcpyAsync(out->Sn, ws.sn, (size_t)ns * V * 4, hipMemcpyDeviceToDevice, st);
       if (out->alpha_ab != nullptr)

@@ -64,7 +64,8 @@ class EngineError(RuntimeError):
     """The engine rejected a call (bad sizes, workspace, launch failure)."""
 
 
-MAX_VALIDATORS = 1024  # include/yuma_hip.h YUMA_MAX_VALIDATORS (register-resident validator columns)
+MAX_VALIDATORS = 1 << 20  # include/yuma_hip.h YUMA_MAX_VALIDATORS
+REG_VALIDATORS = 1024  # YUMA_REG_VALIDATORS: above it the engine streams each miner column
 MAX_BISECT_ITERS = 30  # consensus_precision <= 2**30: the search grid k / 2**iters in int32
 
 
@@ -74,7 +75,7 @@ def check_limits(V: int, M: int) -> None:
     (DESIGN.md §3 'Limits')."""
     if V > MAX_VALIDATORS:
         raise EngineError(f"{V} validators exceed the engine's limit of {MAX_VALIDATORS} per subnet "
-                          "(YUMA_MAX_VALIDATORS: a miner column is held in registers by one workgroup)")
+                          "(YUMA_MAX_VALIDATORS)")
     if M > (1 << 20) * 64:
         raise EngineError(f"{M} miners exceed the engine's limit of {(1 << 20) * 64} (2^20 tiles of 64)")
 
