@@ -24,7 +24,7 @@ Prints ONE JSON line (rank 0) with the driver's fields plus
                 BYTES(V,M) (the fp32 epoch-step contract, 12,617,728 B at
                 256 x 4096), frac = achieved / 8 TB/s; traffic = the rocprofv3
                 FETCH_SIZE + WRITE_SIZE bytes of one step (committed PMC passes of
-                this exact workload, profiles/r04/pmc_traffic.json), and
+                this exact workload, profiles/r05/pmc_traffic.json), and
                 roofline.kernel = the dominant kernel (k_bonds_elem at c2):
                 algorithmic bytes per launch / its HIP-event launch time;
   cpu_baseline  the torch-CPU restatement of the epoch (oracle/torch_cpu.py,
@@ -113,11 +113,13 @@ def kernel_of(phase: str, variant: int, shared: bool = False, V: int = 256, M: i
         return "k_bonds_cn" if V > 64 and M % 4 == 0 else "k_bonds"
     if phase == "consensus" and 64 < V <= 256 and M % 4 == 0 and not shared:
         return "k_consensus_p"  # 128-byte row segments (wave pairs; run outputs)
+    if phase == "rank" and ((variant in (1, 2) and V > 64) or M >= 16384):
+        return "k_rank_sw"  # 256-miner column blocks (bond column sums; wide subnets)
     return PHASE_KERNELS[phase]
 
 
-TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r04", "pmc_traffic.json")
-SQ_JSON = os.path.join(ROOT, "profiles", "r04", "sq_valu.json")
+TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r05", "pmc_traffic.json")
+SQ_JSON = os.path.join(ROOT, "profiles", "r05", "sq_valu.json")
 VALU_PEAK_GINST = 1024 * 2.4 / 2  # G wave64 VALU instructions/s: 1024 SIMDs, 2 cycles each, 2.4 GHz
 
 

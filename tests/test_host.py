@@ -298,7 +298,9 @@ def test_bench_line_helpers():
     assert bench.kernel_of("bonds", engine.VARIANT_YUMA2) == "k_bonds_elem"
     assert bench.kernel_of("bonds", engine.VARIANT_RUST) == "k_bonds_cn"
     assert bench.kernel_of("bonds", engine.VARIANT_YUMA1, V=64) == "k_bonds"  # below 65 validators
-    assert bench.kernel_of("rank", engine.VARIANT_YUMA2) == "k_rank_s"
+    assert bench.kernel_of("rank", engine.VARIANT_YUMA3) == "k_rank_s"
+    assert bench.kernel_of("rank", engine.VARIANT_YUMA2) == "k_rank_sw"  # + bond column sums
+    assert bench.kernel_of("rank", engine.VARIANT_YUMA3, M=65536) == "k_rank_sw"
     assert bench.kernel_of("consensus", engine.VARIANT_YUMA3) == "k_consensus_p"
     assert bench.kernel_of("consensus", engine.VARIANT_YUMA4, shared=True, N=512) == "k_consensus_w"
     assert bench.kernel_of("consensus", engine.VARIANT_YUMA3, V=64) == "k_consensus_w"
@@ -312,7 +314,7 @@ def test_bench_line_helpers():
     assert c3 is not None and "k_bonds_grp" in c3
     c4 = bench.load_traffic({"V": 256, "M": 65536, "epochs": 100, "scenarios_per_gpu": 1,
                              "version": "Yuma 3 (Rhef)", "bond_history": False})
-    assert c4 is not None and "k_consensus_p" in c4  # 128-byte row segments (round 4)
+    assert c4 is not None and "k_consensus_p" in c4 and "k_rank_sw" in c4  # round-5 kernels
     assert bench.load_traffic(dict(key, M=1)) is None
     assert bench.contract_bytes(256, 4096, 3) == 12_617_728
 
