@@ -277,3 +277,12 @@ PATCHES["hist_cb2048"] = [("                               512, 1024, yk::DP_VQ>
 # round 5: YumaRust's strip scan with 2 / 4 waves per 16-miner strip block
 # (cn_w2 / cn_w4: launch_cn<VARIANT, 8, 2> / <VARIANT, 4, 4> at 256 validators;
 # bonds 3.50 -> 9.12 / 5.11 ms, rejected, profiles/r05/ab_cn_waves.txt)
+# Yuma / Yuma2 wide history scan without k_rowsum's screened reciprocal (per-row IEEE 1/rs + per-element guard)
+PATCHES["elem_norq"] = [("constexpr bool kElemRq(int variant, bool hist) { return hist && variant <= YUMA_VARIANT_YUMA2; }",
+                          "constexpr bool kElemRq(int variant, bool hist) { return false; }")]
+# ... and every elem scan (Yuma 3 / 4 history, the history-less c4 / c2 forms): rejected,
+# c2 Yuma 3 bonds 1.58 -> 1.80 ms, c4 1.34 -> 1.65 (profiles/r05/ab_elem_rq.txt)
+PATCHES["elem_rq_all"] = [("constexpr bool kElemRq(int variant, bool hist) { return hist && variant <= YUMA_VARIANT_YUMA2; }",
+                           "constexpr bool kElemRq(int variant, bool hist) { return true; }")]
+PATCHES["elem_rq_nohist"] = [("constexpr bool kElemRq(int variant, bool hist) { return hist && variant <= YUMA_VARIANT_YUMA2; }",
+                              "constexpr bool kElemRq(int variant, bool hist) { return hist ? variant <= YUMA_VARIANT_YUMA2 : true; }")]

@@ -3724,7 +3724,7 @@ __global__ __launch_bounds__(256) void k_rust_big_norm(BondArgs A, int t, const 
 // 4 rows x 256 B (CB = 64) or 1 row x 1 KiB (CB >= 256). The dividend partial
 // of each 64-miner tile is the 16-lane DPP sum of one DPP row in every shape.
 template <int VARIANT, int R, bool VEC, int P, bool VECI, bool NT = false, int BS = 256, int CB = 64,
-          int DPL = DP_TV>
+          int DPL = DP_TV, bool RQ = false>
 __global__ __launch_bounds__(BS, 1) void k_bonds_elem(BondArgs A) {
   constexpr int LPR = CB / 4, G = BS / LPR;
   static_assert(CB % 64 == 0 && BS % LPR == 0, "a 16-lane DPP row must cover one 64-miner tile");
@@ -3809,6 +3809,7 @@ __global__ __launch_bounds__(BS, 1) void k_bonds_elem(BondArgs A) {
 
   float rw[P][R][4], rd[P][R], rsn[P][R], ri[P][4], rba[P][4];
   float rcc[COLNORM ? P : 1][4], rcs[COLNORM ? P : 1][4], rcr[COLNORM ? P : 1][4];  // Yuma / Yuma2: C, csb, csr
+  float rrq[RQ ? P : 1][RQ ? R : 1];  // RQ: k_rowsum's screened RN(1 / row sum) (rq4.y)
   // DP_QTE: the quad partials of up to kQBuf epochs parked in LDS (one float
   // per wave row and epoch) and written out as contiguous runs when the
   // buffer fills or the launch ends: no global store inside the epoch loop
@@ -3826,8 +3827,15 @@ __global__ __launch_bounds__(BS, 1) void k_bonds_elem(BondArgs A) {
       // (rowsum / consensus / rank read it in their own launches): non-
       // temporal loads (c4 bonds 1.63 -> 1.50 ms, same box)
       load4c<VEC, DPL == DP_QTE>(A.W + (A.wsh ? (long long)t : slice) * VM, rr, V, m, M, rw[k][i]);
-      rd[k][i] = A.rsd[slice * V + rr];
-      rsn[k][i] = A.sn[slice * V + rr];
+      if constexpr (RQ) {  // {row sum, screened reciprocal, stake}: one load per row
+        const float4 q = A.rq4[(A.wsh ? (long long)t : slice) * V + rr];
+        rd[k][i] = q.x;
+        rrq[k][i] = q.y;
+        rsn[k][i] = q.z;
+      } else {
+        rd[k][i] = A.rsd[slice * V + rr];
+        rsn[k][i] = A.sn[slice * V + rr];
+      }
     }
     // columns >= M never reach an output
     if (VECI) {
@@ -3885,6 +3893,13 @@ __global__ __launch_bounds__(BS, 1) void k_bonds_elem(BondArgs A) {
         for (int c = 0; c < 4; ++c) ok &= rcr[k][c] == rcr[k][c];
         cfast = __all(ok);
       }
+      bool rfast = false;
+      if constexpr (RQ) {
+        bool ok = true;
+#pragma unroll
+        for (int i = 0; i < R; ++i) ok &= rrq[k][i] == rrq[k][i];
+        rfast = __all(ok);
+      }
 #pragma unroll
       for (int i = 0; i < R; ++i) {
         const int row = row0 + G * i;
@@ -3907,14 +3922,27 @@ __global__ __launch_bounds__(BS, 1) void k_bonds_elem(BondArgs A) {
         // per-element guard: c2 wide history scan 1.58 -> 1.70 ms, c4 1.63 ->
         // 1.73, same box; kept only in the issue-bound sweep scan k_bonds_grp)
         float wn[4];
-        const RowDiv rdv = row_div(rd[k][i]);
-        bool slow = false;
+        if (RQ && rfast) {
+          // every row of the wave passed k_rowsum's screen: RN(w / rs) from
+          // RN(1 / rs) with RowDiv's correction, no per-element guard
 #pragma unroll
-        for (int c = 0; c < 4; ++c)
-          wn[c] = SHORT ? div_fast_nz(rw[k][i][c], rdv, slow) : div_fast(rw[k][i][c], rdv, slow);
-        if (__any(slow)) {
+          for (int c = 0; c < 4; ++c) {
+            const float a = rw[k][i][c];
+            const float q = a * rrq[k][i];
+            const float e = fmaf(-rd[k][i], q, a);
+            const float q1 = fmaf(e, rrq[k][i], q);
+            wn[c] = SHORT ? q1 : (a == 0.0f ? q : q1);
+          }
+        } else {
+          const RowDiv rdv = row_div(rd[k][i]);
+          bool slow = false;
 #pragma unroll
-          for (int c = 0; c < 4; ++c) wn[c] = rw[k][i][c] / rd[k][i];
+          for (int c = 0; c < 4; ++c)
+            wn[c] = SHORT ? div_fast_nz(rw[k][i][c], rdv, slow) : div_fast(rw[k][i][c], rdv, slow);
+          if (__any(slow)) {
+#pragma unroll
+            for (int c = 0; c < 4; ++c) wn[c] = rw[k][i][c] / rd[k][i];
+          }
         }
         if constexpr (COLNORM) {
           // B = nan_to_num(S·W_b / Σ_v S·W_b), W_b = (1-β)·src + β·min(src, C)
@@ -5119,23 +5147,31 @@ constexpr int kWidePCn = 2;    // ... for Yuma / Yuma2 (more work per epoch)
 // 1.33 ms with 3 against 2, profiles/r05/ab_c4_scan.txt)
 constexpr int kNoHistP2 = 3;
 constexpr int kScanGroup = 4;  // scenarios per block of the shared-input scan
+// the scans that divide W by k_rowsum's screened reciprocal (rq4) instead of
+// a per-row IEEE reciprocal and a per-element guard: the Yuma / Yuma2 wide
+// history scan (Yuma 1 bonds 1.84 -> 1.73 ms, same box)
+constexpr bool kElemRq(int variant, bool hist) { return hist && variant <= YUMA_VARIANT_YUMA2; }
 int bonds_rows(bool vec, bool hist, bool wsh) { return vec && (hist || wsh) ? 2 : 1; }
-template <int VARIANT, int R, bool VEC, int P, bool VECI, bool NT, int BS, int CB, int DPL>
+template <int VARIANT, int R, bool VEC, int P, bool VECI, bool NT, int BS, int CB, int DPL, bool RQ = false>
 int launch_elem_shape(hipStream_t st, yk::BondArgs& A) {
   constexpr int G = BS / (CB / 4);
   A.rowblocks = (A.V + G * R - 1) / (G * R);
   A.cblocks = (A.M + CB - 1) / CB;
   const long long nblocks = (long long)A.N * A.rowblocks * A.cblocks;
-  YK_LAUNCH((yk::k_bonds_elem<VARIANT, R, VEC, P, VECI, NT, BS, CB, DPL>), nblocks, BS, st, A);
+  YK_LAUNCH((yk::k_bonds_elem<VARIANT, R, VEC, P, VECI, NT, BS, CB, DPL, RQ>), nblocks, BS, st, A);
   return DPL;
 }
 template <int VARIANT, bool VEC>
 int launch_bonds_elem(hipStream_t st, yk::BondArgs& A) {
   const bool hist = A.B_hist != nullptr;
   if constexpr (VEC) {
-    if (hist && A.M >= 1024)
-      return launch_elem_shape<VARIANT, 2, true, VARIANT <= YUMA_VARIANT_YUMA2 ? kWidePCn : kWideP, true, true,
-                               512, 1024, yk::DP_VQ>(st, A);
+    if (hist && A.M >= 1024) {
+      constexpr int P = VARIANT <= YUMA_VARIANT_YUMA2 ? kWidePCn : kWideP;
+      if constexpr (kElemRq(VARIANT, true)) {
+        if (A.rq4 != nullptr) return launch_elem_shape<VARIANT, 2, true, P, true, true, 512, 1024, yk::DP_VQ, true>(st, A);
+      }
+      return launch_elem_shape<VARIANT, 2, true, P, true, true, 512, 1024, yk::DP_VQ>(st, A);
+    }
   }
   if constexpr (VEC && VARIANT >= YUMA_VARIANT_YUMA3) {
     if (A.wsh && A.N >= 2 && A.rq4 != nullptr) {  // a sweep over one input trajectory
@@ -5155,6 +5191,13 @@ int launch_bonds_elem(hipStream_t st, yk::BondArgs& A) {
     // flight) once the grid has blocks to spare: c4 1.41 -> 1.38 ms; with
     // c2's 512 such blocks 0.99 -> 1.31, so one row per lane there
     const long long blocks_r2 = (long long)A.N * ((A.V + 7) / 8) * ((A.M + 255) / 256);
+    if constexpr (VEC && kElemRq(VARIANT, false)) {
+      if (A.rq4 != nullptr) {
+        if (blocks_r2 >= 4096)
+          return launch_elem_shape<VARIANT, 2, VEC, kNoHistP2, VEC, false, 256, 256, yk::DP_QTE, true>(st, A);
+        return launch_elem_shape<VARIANT, 1, VEC, 4, VEC, false, 256, 256, yk::DP_QTE, true>(st, A);
+      }
+    }
     if (blocks_r2 >= 4096)
       return launch_elem_shape<VARIANT, 2, VEC, kNoHistP2, VEC, false, 256, 256, yk::DP_QTE>(st, A);
     return launch_elem_shape<VARIANT, 1, VEC, 4, VEC, false, 256, 256, yk::DP_QTE>(st, A);
