@@ -286,3 +286,7 @@ PATCHES["elem_rq_all"] = [("constexpr bool kElemRq(int variant, bool hist) { ret
                            "constexpr bool kElemRq(int variant, bool hist) { return true; }")]
 PATCHES["elem_rq_nohist"] = [("constexpr bool kElemRq(int variant, bool hist) { return hist && variant <= YUMA_VARIANT_YUMA2; }",
                               "constexpr bool kElemRq(int variant, bool hist) { return hist ? variant <= YUMA_VARIANT_YUMA2 : true; }")]
+# (round 5, rejected and removed: graph captures issuing the input-only phases
+# of each of 4 / 8 / 16 pieces on a side stream, so consensus / rank of piece
+# k + 1 ran beside the bond scan of piece k: c2 3.80 -> 3.88 / 3.98 / 4.27 ms,
+# c3 7.83 -> 8.42, c4 +- 0; profiles/r05/ab_pipeline.txt)
