@@ -290,3 +290,18 @@ PATCHES["elem_rq_nohist"] = [("constexpr bool kElemRq(int variant, bool hist) { 
 # of each of 4 / 8 / 16 pieces on a side stream, so consensus / rank of piece
 # k + 1 ran beside the bond scan of piece k: c2 3.80 -> 3.88 / 3.98 / 4.27 ms,
 # c3 7.83 -> 8.42, c4 +- 0; profiles/r05/ab_pipeline.txt)
+# k_consensus_p timing-only builds (round 5): no histogram atomics / return
+# after the load + division (results wrong by design)
+PATCHES["diag_consp_noatomic"] = [(
+    "          atomicAdd(hp + (col + c) * kHS + (k < w[c] ? k : w[c]), su);",
+    "          if (su == 0x7FFFFFFFu) atomicAdd(hp + (col + c) * kHS + (k < w[c] ? k : w[c]), su);")]
+PATCHES["diag_consp_loadonly"] = [(
+    "  const int col = cq * 4;  // this lane's first column within the pair's 32\n",
+    "  const int col = cq * 4;  // this lane's first column within the pair's 32\n"
+    "  {\n    float t = 0.0f;\n    for (int i = 0; i < R; ++i) for (int c = 0; c < 4; ++c) t = t + wn[i][c];\n"
+    "    if (t == 1234.5f) craw[slice * M + m] = t;\n    return;\n  }\n")]
+# (round 5, rejected and removed: k_consensus_pf, a persistent form of
+# k_consensus_p at 2 blocks / CU issuing the next tile's W rows (4 / 8 / 12 /
+# 16 of 16 per lane) before each search: consensus 0.85 -> 1.02 / 1.05 /
+# 1.19 / 1.30 ms; the search needs the third wave per SIMD more than the
+# loads need the lead; profiles/r05/ab_consensus_pf.txt)
