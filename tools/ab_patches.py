@@ -305,3 +305,6 @@ PATCHES["diag_consp_loadonly"] = [(
 # 16 of 16 per lane) before each search: consensus 0.85 -> 1.02 / 1.05 /
 # 1.19 / 1.30 ms; the search needs the third wave per SIMD more than the
 # loads need the lead; profiles/r05/ab_consensus_pf.txt)
+# (round 5, rejected and removed: k_consensus_p's histogram widened from 64
+# to 96 / 128 grid points, so c2's brackets (<= 65 points) finish without a
+# bisection pass: consensus 0.85 -> 0.855 / 0.87-0.88; profiles/r05/ab_hist_bins.txt)
