@@ -278,14 +278,13 @@ PATCHES["hist_cb2048"] = [("                               512, 1024, yk::DP_VQ>
 # (cn_w2 / cn_w4: launch_cn<VARIANT, 8, 2> / <VARIANT, 4, 4> at 256 validators;
 # bonds 3.50 -> 9.12 / 5.11 ms, rejected, profiles/r05/ab_cn_waves.txt)
 # Yuma / Yuma2 wide history scan without k_rowsum's screened reciprocal (per-row IEEE 1/rs + per-element guard)
-PATCHES["elem_norq"] = [("constexpr bool kElemRq(int variant, bool hist) { return hist && variant <= YUMA_VARIANT_YUMA2; }",
-                          "constexpr bool kElemRq(int variant, bool hist) { return false; }")]
+PATCHES["elem_norq"] = [("constexpr bool kElemRq(int variant, bool hist) { return hist ? variant <= YUMA_VARIANT_YUMA2 : true; }",
+                          "constexpr bool kElemRq(int variant, bool hist) { return false; }"),
+                         ("constexpr int kNoHistP2 = 2;", "constexpr int kNoHistP2 = 3;")]
 # ... and every elem scan (Yuma 3 / 4 history, the history-less c4 / c2 forms): rejected,
 # c2 Yuma 3 bonds 1.58 -> 1.80 ms, c4 1.34 -> 1.65 (profiles/r05/ab_elem_rq.txt)
-PATCHES["elem_rq_all"] = [("constexpr bool kElemRq(int variant, bool hist) { return hist && variant <= YUMA_VARIANT_YUMA2; }",
+PATCHES["elem_rq_all"] = [("constexpr bool kElemRq(int variant, bool hist) { return hist ? variant <= YUMA_VARIANT_YUMA2 : true; }",
                            "constexpr bool kElemRq(int variant, bool hist) { return true; }")]
-PATCHES["elem_rq_nohist"] = [("constexpr bool kElemRq(int variant, bool hist) { return hist && variant <= YUMA_VARIANT_YUMA2; }",
-                              "constexpr bool kElemRq(int variant, bool hist) { return hist ? variant <= YUMA_VARIANT_YUMA2 : true; }")]
 # (round 5, rejected and removed: graph captures issuing the input-only phases
 # of each of 4 / 8 / 16 pieces on a side stream, so consensus / rank of piece
 # k + 1 ran beside the bond scan of piece k: c2 3.80 -> 3.88 / 3.98 / 4.27 ms,
@@ -308,3 +307,7 @@ PATCHES["diag_consp_loadonly"] = [(
 # (round 5, rejected and removed: k_consensus_p's histogram widened from 64
 # to 96 / 128 grid points, so c2's brackets (<= 65 points) finish without a
 # bisection pass: consensus 0.85 -> 0.855 / 0.87-0.88; profiles/r05/ab_hist_bins.txt)
+# (round 5: the first history-less form loaded {row sum, reciprocal, stake} as
+# one 16-byte rq4 record; the compiler copied the reciprocal out of the load's
+# register tuple right after issuing it and waited vmcnt(0) each epoch: c4
+# bonds 1.25 -> 1.58. The reciprocal is now its own 4-byte load.)

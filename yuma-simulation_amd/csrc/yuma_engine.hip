@@ -3827,15 +3827,13 @@ __global__ __launch_bounds__(BS, 1) void k_bonds_elem(BondArgs A) {
       // (rowsum / consensus / rank read it in their own launches): non-
       // temporal loads (c4 bonds 1.63 -> 1.50 ms, same box)
       load4c<VEC, DPL == DP_QTE>(A.W + (A.wsh ? (long long)t : slice) * VM, rr, V, m, M, rw[k][i]);
-      if constexpr (RQ) {  // {row sum, screened reciprocal, stake}: one load per row
-        const float4 q = A.rq4[(A.wsh ? (long long)t : slice) * V + rr];
-        rd[k][i] = q.x;
-        rrq[k][i] = q.y;
-        rsn[k][i] = q.z;
-      } else {
-        rd[k][i] = A.rsd[slice * V + rr];
-        rsn[k][i] = A.sn[slice * V + rr];
-      }
+      rd[k][i] = A.rsd[slice * V + rr];
+      rsn[k][i] = A.sn[slice * V + rr];
+      // RQ: the screened reciprocal alone (rq4.y). (One 16-byte rq4 load for
+      // all three made the compiler copy the reciprocal out of the load's
+      // register tuple right after the load, waiting vmcnt(0) at every
+      // epoch: c4 bonds 1.25 -> 1.58 ms.)
+      if constexpr (RQ) rrq[k][i] = reinterpret_cast<const float*>(A.rq4)[((A.wsh ? (long long)t : slice) * V + rr) * 4 + 1];
     }
     // columns >= M never reach an output
     if (VECI) {
@@ -3893,13 +3891,6 @@ __global__ __launch_bounds__(BS, 1) void k_bonds_elem(BondArgs A) {
         for (int c = 0; c < 4; ++c) ok &= rcr[k][c] == rcr[k][c];
         cfast = __all(ok);
       }
-      bool rfast = false;
-      if constexpr (RQ) {
-        bool ok = true;
-#pragma unroll
-        for (int i = 0; i < R; ++i) ok &= rrq[k][i] == rrq[k][i];
-        rfast = __all(ok);
-      }
 #pragma unroll
       for (int i = 0; i < R; ++i) {
         const int row = row0 + G * i;
@@ -3922,9 +3913,10 @@ __global__ __launch_bounds__(BS, 1) void k_bonds_elem(BondArgs A) {
         // per-element guard: c2 wide history scan 1.58 -> 1.70 ms, c4 1.63 ->
         // 1.73, same box; kept only in the issue-bound sweep scan k_bonds_grp)
         float wn[4];
-        if (RQ && rfast) {
-          // every row of the wave passed k_rowsum's screen: RN(w / rs) from
-          // RN(1 / rs) with RowDiv's correction, no per-element guard
+        if constexpr (RQ) {
+          // RN(w / rs) from k_rowsum's screened RN(1 / rs) with RowDiv's
+          // correction and no per-element guard; a row that failed the
+          // screen (NaN reciprocal) sends the wave to IEEE division
 #pragma unroll
           for (int c = 0; c < 4; ++c) {
             const float a = rw[k][i][c];
@@ -3932,6 +3924,10 @@ __global__ __launch_bounds__(BS, 1) void k_bonds_elem(BondArgs A) {
             const float e = fmaf(-rd[k][i], q, a);
             const float q1 = fmaf(e, rrq[k][i], q);
             wn[c] = SHORT ? q1 : (a == 0.0f ? q : q1);
+          }
+          if (__any(rrq[k][i] != rrq[k][i])) {
+#pragma unroll
+            for (int c = 0; c < 4; ++c) wn[c] = rw[k][i][c] / rd[k][i];
           }
         } else {
           const RowDiv rdv = row_div(rd[k][i]);
@@ -5144,13 +5140,16 @@ int launch_bonds_colnorm(RowCfg rc, hipStream_t st, yk::BondArgs& A, int* ptiles
 constexpr int kWideP = 2;      // epochs in flight of the wide history scan
 constexpr int kWidePCn = 2;    // ... for Yuma / Yuma2 (more work per epoch)
 // epochs in flight of the two-row history-less scan (c4 bonds 1.37-1.39 ->
-// 1.33 ms with 3 against 2, profiles/r05/ab_c4_scan.txt)
-constexpr int kNoHistP2 = 3;
+// 1.33 ms with 3 against 2 with the guarded division, profiles/r05/ab_c4_scan.txt;
+// with the screened reciprocal 2: 1.25-1.27 against 1.32-1.36 at 3)
+constexpr int kNoHistP2 = 2;
 constexpr int kScanGroup = 4;  // scenarios per block of the shared-input scan
 // the scans that divide W by k_rowsum's screened reciprocal (rq4) instead of
 // a per-row IEEE reciprocal and a per-element guard: the Yuma / Yuma2 wide
-// history scan (Yuma 1 bonds 1.84 -> 1.73 ms, same box)
-constexpr bool kElemRq(int variant, bool hist) { return hist && variant <= YUMA_VARIANT_YUMA2; }
+// history scan (Yuma 1 bonds 1.84 -> 1.73 ms, same box) and the history-less
+// forms (c4 1.32-1.33 -> 1.25-1.27 with 2 epochs in flight, c2 --no-history
+// 0.985-0.997 -> 0.916-0.923; profiles/r05/ab_elem_rq.txt)
+constexpr bool kElemRq(int variant, bool hist) { return hist ? variant <= YUMA_VARIANT_YUMA2 : true; }
 int bonds_rows(bool vec, bool hist, bool wsh) { return vec && (hist || wsh) ? 2 : 1; }
 template <int VARIANT, int R, bool VEC, int P, bool VECI, bool NT, int BS, int CB, int DPL, bool RQ = false>
 int launch_elem_shape(hipStream_t st, yk::BondArgs& A) {
