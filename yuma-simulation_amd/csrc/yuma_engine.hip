@@ -4175,6 +4175,13 @@ __device__ __forceinline__ void grp_scan(const BondArgs& A, unsigned liquid_mask
     fW[i] = A.W + (long long)A.t0 * VM + (long long)rr * M + mc;
     fQ[i] = A.rq4 + (long long)A.t0 * V + rr;
   }
+  // (the record's three fields as three 4-byte loads, the reciprocal with the
+  // non-temporal hint so that they are not merged into one: from one 16-byte
+  // load the compiler copied the fields out of the load's register tuple
+  // right after issuing it and waited vmcnt(0) there, every epoch)
+  // (Unconditional refills from clamped addresses instead of the skipped
+  // loads past the last epoch: 149-168 VGPRs and spills, the latch's drain
+  // stayed.)
   auto fetch = [&](int kk, bool load) {
 #pragma unroll
     for (int i = 0; i < R; ++i) {
@@ -4184,10 +4191,10 @@ __device__ __forceinline__ void grp_scan(const BondArgs& A, unsigned liquid_mask
         rw[kk][i][1] = x.y;
         rw[kk][i][2] = x.z;
         rw[kk][i][3] = x.w;
-        const float4 q = *fQ[i];
-        rd[kk][i] = q.x;
-        rq[kk][i] = q.y;
-        rsn[kk][i] = q.z;
+        const float* q = reinterpret_cast<const float*>(fQ[i]);
+        rd[kk][i] = q[0];
+        rq[kk][i] = __builtin_nontemporal_load(q + 1);
+        rsn[kk][i] = q[2];
       }
       fW[i] += VM;
       fQ[i] += V;
@@ -4288,20 +4295,19 @@ __device__ __forceinline__ void grp_scan(const BondArgs& A, unsigned liquid_mask
       // from the stored reciprocal when every row of the wave is in range,
       // else IEEE division (the same values up to the sign of a zero)
       float wn[R][4];
-      bool fast = true;
+      bool slow = false;
 #pragma unroll
-      for (int i = 0; i < R; ++i) fast &= rq[kk][i] == rq[kk][i];
-      if (__all(fast)) {
+      for (int i = 0; i < R; ++i) {
+        slow |= rq[kk][i] != rq[kk][i];
 #pragma unroll
-        for (int i = 0; i < R; ++i)
-#pragma unroll
-          for (int c = 0; c < 4; ++c) {
-            const float a = rw[kk][i][c];
-            const float q = a * rq[kk][i];
-            const float e = fmaf(-rd[kk][i], q, a);
-            wn[i][c] = fmaf(e, rq[kk][i], q);
-          }
-      } else {
+        for (int c = 0; c < 4; ++c) {
+          const float a = rw[kk][i][c];
+          const float q = a * rq[kk][i];
+          const float e = fmaf(-rd[kk][i], q, a);
+          wn[i][c] = fmaf(e, rq[kk][i], q);
+        }
+      }
+      if (__any(slow)) {  // (tested after the division: a test ahead of it drained the ring)
 #pragma unroll
         for (int i = 0; i < R; ++i)
 #pragma unroll
@@ -4367,10 +4373,12 @@ __device__ __forceinline__ void grp_scan(const BondArgs& A, unsigned liquid_mask
           if (hist && row < V && m < M)
             *reinterpret_cast<float4*>(pH[k] + (long long)G * i * M) =
                 make_float4(B[k][i][0], B[k][i][1], B[k][i][2], B[k][i][3]);
+          // (a select, not a lane branch: the branch made the compiler wait
+          // vmcnt(0) inside it, draining the W ring)
           float d = 0.0f;
-          if (m < M)
 #pragma unroll
-            for (int c = 0; c < 4; ++c) d = d + B[k][i][c] * ic[c];
+          for (int c = 0; c < 4; ++c) d = d + B[k][i][c] * ic[c];
+          d = m < M ? d : 0.0f;
           d = wsum16(d);
           if constexpr (kGrpPark) {
             if (L.c4 == 0) dpb[(((t - tq) * K + k) * R + i) * 4 + (L.lane >> 4)] = d;
