@@ -4182,22 +4182,25 @@ __device__ __forceinline__ void grp_scan(const BondArgs& A, unsigned liquid_mask
   // (Unconditional refills from clamped addresses instead of the skipped
   // loads past the last epoch: 149-168 VGPRs and spills, the latch's drain
   // stayed.)
-  auto fetch = [&](int kk, bool load) {
+  // Every ring load is unconditional: the pointers hold the next epoch to
+  // fetch, clamped at the last one (a fetch past the end re-reads it), and
+  // advance only while epochs remain (`more`, block-uniform). (Loads skipped
+  // on some path left the waitcnt pass no count for the older ones but
+  // vmcnt(0).)
+  auto fetch = [&](int kk, bool more) {
 #pragma unroll
     for (int i = 0; i < R; ++i) {
-      if (load) {
-        const float4 x = *reinterpret_cast<const float4*>(fW[i]);
-        rw[kk][i][0] = x.x;
-        rw[kk][i][1] = x.y;
-        rw[kk][i][2] = x.z;
-        rw[kk][i][3] = x.w;
-        const float* q = reinterpret_cast<const float*>(fQ[i]);
-        rd[kk][i] = q[0];
-        rq[kk][i] = __builtin_nontemporal_load(q + 1);
-        rsn[kk][i] = q[2];
-      }
-      fW[i] += VM;
-      fQ[i] += V;
+      const float4 x = *reinterpret_cast<const float4*>(fW[i]);
+      rw[kk][i][0] = x.x;
+      rw[kk][i][1] = x.y;
+      rw[kk][i][2] = x.z;
+      rw[kk][i][3] = x.w;
+      const float* q = reinterpret_cast<const float*>(fQ[i]);
+      rd[kk][i] = q[0];
+      rq[kk][i] = __builtin_nontemporal_load(q + 1);
+      rsn[kk][i] = q[2];
+      fW[i] += more ? VM : 0;
+      fQ[i] += more ? V : 0;
     }
   };
   // per scenario: incentive (and liquid bond_alpha) of the epoch in use, each
@@ -4216,28 +4219,26 @@ __device__ __forceinline__ void grp_scan(const BondArgs& A, unsigned liquid_mask
     pD[k] = A.dpart + (s0 * A.tiles + tile) * V + row0;
     pH[k] = hist ? A.B_hist + s0 * VM + (long long)row0 * M + m : nullptr;
   }
-  auto fetch_s = [&](int k, bool load) {
-    if (load) {
-      const float4 x = *reinterpret_cast<const float4*>(fI[k]);
-      ri[k][0] = x.x;
-      ri[k][1] = x.y;
-      ri[k][2] = x.z;
-      ri[k][3] = x.w;
-      if (LQ == 2 || (LQ == 1 && ((liquid_mask >> k) & 1u))) {
-        const float4 y = *reinterpret_cast<const float4*>(fB[k]);
-        rba[k][0] = y.x;
-        rba[k][1] = y.y;
-        rba[k][2] = y.z;
-        rba[k][3] = y.w;
-      }
+  auto fetch_s = [&](int k, bool more) {  // as fetch: unconditional, clamped
+    const float4 x = *reinterpret_cast<const float4*>(fI[k]);
+    ri[k][0] = x.x;
+    ri[k][1] = x.y;
+    ri[k][2] = x.z;
+    ri[k][3] = x.w;
+    if (LQ == 2 || (LQ == 1 && ((liquid_mask >> k) & 1u))) {
+      const float4 y = *reinterpret_cast<const float4*>(fB[k]);
+      rba[k][0] = y.x;
+      rba[k][1] = y.y;
+      rba[k][2] = y.z;
+      rba[k][3] = y.w;
     }
-    fI[k] += sM;
-    fB[k] += sM;
+    fI[k] += more ? sM : 0;
+    fB[k] += more ? sM : 0;
   };
 #pragma unroll
-  for (int kk = 0; kk < P; ++kk) fetch(kk, A.t0 + kk < A.t1);
+  for (int kk = 0; kk < P; ++kk) fetch(kk, A.t0 + kk + 1 < A.t1);
 #pragma unroll
-  for (int k = 0; k < K; ++k) fetch_s(k, true);
+  for (int k = 0; k < K; ++k) fetch_s(k, A.t0 + 1 < A.t1);
   // Liquid blocks: a fixed-alpha scenario keeps bond_alpha in rba for the
   // whole scan, and one_minus_bond_alpha = (1 - bond_alpha) + p_corr. Both
   // terms of p_corr are fp32 roundings of 1 - bond_alpha within 2^-25 of each
@@ -4386,7 +4387,7 @@ __device__ __forceinline__ void grp_scan(const BondArgs& A, unsigned liquid_mask
             if (L.c4 == 0 && row < V) pD[k][G * i] = d;
           }
         }
-        fetch_s(k, t + 1 < A.t1);
+        fetch_s(k, t + 2 < A.t1);
         pD[k] += sD;
         if (hist) pH[k] += sM * V;
       }
@@ -4394,7 +4395,7 @@ __device__ __forceinline__ void grp_scan(const BondArgs& A, unsigned liquid_mask
       // vmcnt drains in issue order, so waiting for the next epoch's
       // incentive does not wait for the rows two epochs ahead (c3 bonds
       // 6.69-6.73 -> 6.61-6.62 ms, profiles/r05/ab_grp.txt)
-      fetch(kk, t + P < A.t1);
+      fetch(kk, t + P + 1 < A.t1);
       if constexpr (kGrpPark) {
         if (t - tq == kGrpDB - 1 || t == A.t1 - 1) flush_d(t);  // wave-uniform
       }
