@@ -311,3 +311,6 @@ PATCHES["diag_consp_loadonly"] = [(
 # one 16-byte rq4 record; the compiler copied the reciprocal out of the load's
 # register tuple right after issuing it and waited vmcnt(0) each epoch: c4
 # bonds 1.25 -> 1.58. The reciprocal is now its own 4-byte load.)
+# element-wise scan: unconditional clamped ring refill alone (round 5: c2 1.54 -> 1.56, c4 1.27 -> 1.41, rejected)
+PATCHES["elem_refill_clamped"] = [("      if (t + P < A.t1) fetch(k, t + P);\n    }\n  }\n#pragma unroll\n  for (int i = 0; i < R; ++i) {\n    const int row = row0 + G * i;\n    if (row < V) store4<VEC>(A.Bstate",
+                                   "      fetch(k, min(t + P, A.t1 - 1));\n    }\n  }\n#pragma unroll\n  for (int i = 0; i < R; ++i) {\n    const int row = row0 + G * i;\n    if (row < V) store4<VEC>(A.Bstate")]
