@@ -81,13 +81,14 @@ def phase_bytes(phase: str, V: int, M: int, variant: int, liquid: bool, hist: bo
     table = {
         "consensus": w + 8 * V + 8 * M,
         "quantise": 8 * M + 8 * M + (4 * M if liquid else 0),
-        # Yuma / Yuma2 also write the bond column sums csb [M]
-        "rank": w + 8 * V + 4 * M + 4 * M + 4 * tiles + (4 * M if variant in (1, 2) else 0),
+        # Yuma / Yuma2 also write the bond column sums csb [M] and csr [M]
+        "rank": w + 8 * V + 4 * M + 4 * M + 4 * tiles + (8 * M if variant in (1, 2) else 0),
         "rowsum": w + (4 * V + 8 * V + 16 * V) / wshare,
         "incentive": 4 * M + 4 * tiles + 4 * M,
         # column-normalised variants read C and a column sum per miner (Yuma /
-        # Yuma2: csb; YumaRust: its rank R)
-        "bonds": (w + 8 * V + 4 * M + (8 * M if colnorm else 0) + (4 * M if liquid else 0)
+        # Yuma2: csb and its screened reciprocal csr, 12 B; YumaRust: its rank R, 8 B)
+        "bonds": (w + 8 * V + 4 * M + ((12 if variant in (1, 2) else 8) * M if colnorm else 0)
+                  + (4 * M if liquid else 0)
                   + (4 * VM if hist else 0) + 4 * V * ptiles + 8 * VM / max(chunk, 1)),
         "finalize": 4 * V * ptiles + 4 * V + 4 * V,
     }

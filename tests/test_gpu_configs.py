@@ -321,6 +321,16 @@ def test_wide_float_weights_against_oracle():
     (engine.VARIANT_RUST, {"liquid_alpha": True}, None, 4, ("R", "D"), (5, 200)),
     (engine.VARIANT_YUMA1, {}, None, 0, ("R", "D", "T", "Tv"), (6, 130)),
     (engine.VARIANT_YUMA2, {}, None, 3, ("R", "D"), (4, 256)),
+    # Yuma 1 run outputs above 64 validators on shared inputs take
+    # the rank-class dedup (k_classes with bond_penalty) AND the bond column
+    # sums csb / csr of the element-wise scan; a duplicate scenario's scan
+    # reads its representative's csb / csr (κ repeats every 3 scenarios, so
+    # every class has duplicates). 130 validators: k_rank_s; 1100: above
+    # kRegRows, the 256-miner column-block rank k_rank_sw
+    (engine.VARIANT_YUMA1, {}, None, 0, ("R", "D"), (6, 130)),
+    (engine.VARIANT_YUMA1, {"bond_penalty": 0.5}, None, 4, (), (7, 130)),
+    (engine.VARIANT_YUMA1, {"bond_penalty": 0.5}, None, 0, ("R", "D"), (6, 1100)),
+    (engine.VARIANT_YUMA1, {"liquid_alpha": True}, None, 3, (), (5, 1100)),
 ])
 def test_shared_input_sweep_equals_replicated(variant, extra, reset, chunk, want, N):
     """yuma_run_ex(YUMA_RUN_SHARED_INPUTS): N scenarios reading ONE W/S

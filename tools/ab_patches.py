@@ -314,3 +314,17 @@ PATCHES["diag_consp_loadonly"] = [(
 # element-wise scan: unconditional clamped ring refill alone (round 5: c2 1.54 -> 1.56, c4 1.27 -> 1.41, rejected)
 PATCHES["elem_refill_clamped"] = [("      if (t + P < A.t1) fetch(k, t + P);\n    }\n  }\n#pragma unroll\n  for (int i = 0; i < R; ++i) {\n    const int row = row0 + G * i;\n    if (row < V) store4<VEC>(A.Bstate",
                                    "      fetch(k, min(t + P, A.t1 - 1));\n    }\n  }\n#pragma unroll\n  for (int i = 0; i < R; ++i) {\n    const int row = row0 + G * i;\n    if (row < V) store4<VEC>(A.Bstate")]
+
+# ---------------------------------------------------------------------------
+# Round 6: YumaRust's strip scan k_bonds_cn. Timing-only
+# builds on top of the LDS-parked dividend partials:
+#   diag_cn_nohist  no bond-history stores (the launch still asks for them)
+#   diag_cn_nobar   the state-dependent column sum of B_ema from the wave's own
+#                   16 rows only (no LDS hand-off, no block barrier)
+#   diag_cn_noflush partials parked but never written
+_CN_HIST = "        if (A.B_hist != nullptr && row < V && colok)\n          __builtin_nontemporal_store("
+PATCHES["diag_cn_nohist"] = [(_CN_HIST, _CN_HIST.replace("row < V && colok", "row < 0 && colok"))]
+PATCHES["diag_cn_nobar"] = [("        cn_wave_sums<NW>(ema, red[par], cq, rr, wave);",
+                             "        cn_wave_sums<1>(ema, red[par], cq, rr, wave);")]
+PATCHES["diag_cn_noflush"] = [("      if (t - tq == DB - 1 || t == A.t1 - 1) flush_d(t);  // block-uniform",
+                               "      if (t - tq == DB - 1 || t == A.t1 - 1) tq = t + 1;")]
