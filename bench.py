@@ -119,39 +119,52 @@ def kernel_of(phase: str, variant: int, shared: bool = False, V: int = 256, M: i
     return PHASE_KERNELS[phase]
 
 
-TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r05", "pmc_traffic.json")
-SQ_JSON = os.path.join(ROOT, "profiles", "r05", "sq_valu.json")
+TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r06", "pmc_traffic.json")
+SQ_JSON = os.path.join(ROOT, "profiles", "r06", "sq_valu.json")
+
+
+def engine_build_id() -> str:
+    from yuma_simulation._internal import engine
+
+    return engine.build_id()
+
+
+def _matching_record(path: str, key: dict) -> dict | None:
+    """The committed counter record of this exact workload measured on THIS
+    library build (record build_id == yuma_build_id()), else None: a record
+    from another build describes other kernels and is never paired with this
+    run's timings."""
+    try:
+        with open(path) as f:
+            records = json.load(f)
+    except (OSError, ValueError):
+        return None
+    for rec in records:
+        wl = rec.get("workload", {})
+        if all(wl.get(k) == v for k, v in key.items()):
+            return rec if rec.get("build_id") == engine_build_id() else None
+    return None
 VALU_PEAK_GINST = 1024 * 2.4 / 2  # G wave64 VALU instructions/s: 1024 SIMDs, 2 cycles each, 2.4 GHz
 
 
 def load_sq(key: dict) -> dict | None:
     """Per-kernel SQ counts per launch (SQ_INSTS_VALU, ...) of the committed SQ
-    pass of this exact workload (tools/sq_summary.py), or None."""
-    try:
-        with open(SQ_JSON) as f:
-            records = json.load(f)
-    except (OSError, ValueError):
+    pass of this exact workload on this library build (tools/sq_summary.py), or None."""
+    rec = _matching_record(SQ_JSON, key)
+    if rec is None:
         return None
-    for rec in records:
-        wl = rec.get("workload", {})
-        if all(wl.get(k) == v for k, v in key.items()):
-            return {k: dict(v["counters"], commit=rec.get("commit")) for k, v in rec["kernels"].items()}
-    return None
+    return {k: dict(v["counters"], commit=rec.get("commit"), build_id=rec.get("build_id"))
+            for k, v in rec["kernels"].items()}
 
 
 def load_traffic(key: dict) -> dict | None:
     """Per-kernel HBM bytes per scenario-epoch (FETCH_SIZE + WRITE_SIZE,
-    corrected) of the committed PMC passes of this exact workload, or None."""
-    try:
-        with open(TRAFFIC_JSON) as f:
-            records = json.load(f)
-    except (OSError, ValueError):
+    corrected) of the committed PMC passes of this exact workload on this
+    library build, or None."""
+    rec = _matching_record(TRAFFIC_JSON, key)
+    if rec is None:
         return None
-    for rec in records:
-        wl = rec.get("workload", {})
-        if all(wl.get(k) == v for k, v in key.items()):
-            return {k: float(v["hbm_bytes_per_scenario_epoch"]) for k, v in rec["kernels"].items()}
-    return None
+    return {k: float(v["hbm_bytes_per_scenario_epoch"]) for k, v in rec["kernels"].items()}
 
 
 def contract_bytes(V: int, M: int, variant: int) -> float:
@@ -329,6 +342,9 @@ def base_line(args, world: int, value: float, unit: str, elapsed: float, scaling
         "dtype": "f32",
         "data": "synthetic (integer-valued weights, stakes summing to 2^20; SURVEY \u00a78d generator)",
         "config": config,
+        # the library's source identity; counter-derived fields (traffic, the
+        # c3 VALU roofline) are filled only from records of this same build
+        "engine_build_id": engine_build_id(),
     }
 
 
@@ -473,7 +489,7 @@ def engine_line(args, variant: int, params: list, W, S, world: int, dist: bool, 
             "frac": None if ach is None else round(ach / VALU_PEAK_GINST, 4),
             "traffic": None if pmc is None or dom_kernel not in pmc else round(pmc[dom_kernel] * units / launches),
             "definition": (f"{dom_kernel}: SQ_INSTS_VALU per launch ({os.path.relpath(SQ_JSON, ROOT)}, "
-                           f"commit {None if valu is None else valu.get('commit')}) / its HIP-event launch time; "
+                           f"build {None if valu is None else valu.get('build_id')}) / its HIP-event launch time; "
                            f"peak = 1024 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU instruction; traffic = its "
                            "rocprofv3 FETCH_SIZE + WRITE_SIZE bytes per launch (beyond L2, Infinity-Cache hits "
                            "included: W is re-read per scenario pair, not an HBM fraction)"),

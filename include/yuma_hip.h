@@ -290,6 +290,12 @@ int yuma_synth_weights(uint64_t seed, int E, int N, int V, int M, int t0, float*
 
 const char* yuma_last_error(void);
 const char* yuma_version(void);
+/* Build identity of this library: "src-" + the first 16 hex digits of the
+ * SHA-256 of the engine source and this header it was compiled from (stamped
+ * by __graft_entry__.build / tools/ab_build.py; "unstamped" otherwise).
+ * bench.py pairs a committed counter record with a run only when their build
+ * ids match (no reference counterpart: measurement plumbing).               */
+const char* yuma_build_id(void);
 
 #ifdef __cplusplus
 }

@@ -382,3 +382,33 @@ def test_grp_one_minus_alpha_correction():
         if got.view(np.uint32) != want.view(np.uint32):
             bad.append((a, float(got), float(want)))
     assert not bad, bad[:5]
+
+
+def test_library_build_id_is_this_source():
+    """yuma_build_id stamps the SHA-256 prefix of the engine source + header
+    the library was compiled from: the in-tree library is this tree's source
+    (bench.py pairs committed counter records with runs by this id)."""
+    import __graft_entry__ as g
+    from yuma_simulation._internal import engine
+
+    assert engine.build_id() == g.source_build_id()
+
+
+def test_bench_ignores_counter_records_of_another_build(tmp_path, monkeypatch):
+    """a PMC / SQ record measured on another library build
+    is never paired with this run's timings."""
+    import json
+
+    import bench
+
+    key = {"V": 256, "M": 4096, "epochs": 1000, "scenarios_per_gpu": 1, "version": "Yuma 3 (Rhef)",
+           "bond_history": True}
+    rec = {"workload": key, "build_id": "src-0000000000000000",
+           "kernels": {"k_bonds_elem": {"hbm_bytes_per_scenario_epoch": 1.0}}}
+    p = tmp_path / "pmc.json"
+    p.write_text(json.dumps([rec]))
+    monkeypatch.setattr(bench, "TRAFFIC_JSON", str(p))
+    monkeypatch.setattr(bench, "engine_build_id", lambda: "src-1111111111111111")
+    assert bench.load_traffic(key) is None
+    monkeypatch.setattr(bench, "engine_build_id", lambda: "src-0000000000000000")
+    assert bench.load_traffic(key) == {"k_bonds_elem": 1.0}

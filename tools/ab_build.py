@@ -45,7 +45,8 @@ def build(name: str) -> str:
     with open(src, "w") as f:
         f.write(patched(name))
     out = os.path.join(ROOT, "ablib", f"{name}.so")
-    cmd = [os.environ.get("HIPCC", "/opt/rocm/bin/hipcc"), *g.HIPCC_FLAGS, "-w",
+    bid = g.source_build_id(open(src).read())
+    cmd = [os.environ.get("HIPCC", "/opt/rocm/bin/hipcc"), *g.HIPCC_FLAGS, "-w", f'-DYUMA_BUILD_ID="{bid}"',
            "-I", os.path.join(ROOT, "include"), "-o", out, src]
     try:
         subprocess.run(cmd, check=True)

@@ -54,6 +54,20 @@ def counters(directory: str, name: str) -> dict[str, list[float]]:
     return out
 
 
+def bench_build_id(directory: str) -> str | None:
+    """engine_build_id of the bench line a pass ran (its log: <dir>.log or
+    <dir>/run.log, last JSON line)."""
+    for log in (directory.rstrip("/") + ".log", os.path.join(directory, "run.log")):
+        if os.path.exists(log):
+            for line in reversed(open(log).read().splitlines()):
+                if line.startswith("{"):
+                    try:
+                        return json.loads(line).get("engine_build_id")
+                    except ValueError:
+                        continue
+    return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("fetch_dir")
@@ -68,7 +82,14 @@ def main():
                                                   "pmc_traffic.json"))
     ap.add_argument("--commit", default=None, help="git commit of the library the passes ran (ADVICE r3)")
     ap.add_argument("--launches", type=int, default=1, help="launches of each kernel per bench step")
+    ap.add_argument("--build-id", default=None, help="yuma_build_id of the library (default: from the bench logs)")
     a = ap.parse_args()
+    bid = a.build_id
+    if bid is None:
+        ids = {bench_build_id(a.fetch_dir), bench_build_id(a.write_dir)}
+        if len(ids) != 1 or None in ids:
+            raise SystemExit(f"the FETCH and WRITE passes ran different / unknown builds: {ids}")
+        bid = ids.pop()
     fetch = counters(a.fetch_dir, "FETCH_SIZE")
     write = counters(a.write_dir, "WRITE_SIZE")
     units = a.epochs * a.scenarios
@@ -92,6 +113,7 @@ def main():
                      "version": a.version, "bond_history": bool(a.history)},
         "correction": "FETCH_SIZE x2 (gfx950 wide-read half count), KiB -> bytes; WRITE_SIZE as is",
         "commit": a.commit,
+        "build_id": bid,
         "step_hbm_bytes": sum(v["hbm_bytes_per_launch"] for v in kernels.values()) * a.launches,
         "kernels": kernels,
     }

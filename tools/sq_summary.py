@@ -22,7 +22,17 @@ ap.add_argument("--skip", type=int, default=0, help="first dispatches of each ke
 ap.add_argument("--json", default=None, help="append a record to this sq_valu.json (bench.py load_sq)")
 ap.add_argument("--workload", default=None, help='JSON of the bench workload key, e.g. {"V": 256, ...}')
 ap.add_argument("--commit", default=None)
+ap.add_argument("--build-id", default=None, help="yuma_build_id of the library (default: from the bench log)")
 a = ap.parse_args()
+if a.build_id is None:
+    for log in (os.path.join(a.dir, "run.log"), a.dir.rstrip("/") + ".log"):
+        if os.path.exists(log):
+            for line in reversed(open(log).read().splitlines()):
+                if line.startswith("{") and "engine_build_id" in line:
+                    a.build_id = json.loads(line)["engine_build_id"]
+                    break
+        if a.build_id:
+            break
 files = glob.glob(os.path.join(a.dir, "**", "*counter_collection*.csv"), recursive=True)
 if not files:
     raise SystemExit(f"no counter_collection csv under {a.dir}")
@@ -68,5 +78,5 @@ if a.json:
         recs = json.load(open(a.json))
     wl = json.loads(a.workload) if a.workload else {}
     recs = [r for r in recs if r.get("workload") != wl]
-    recs.append({"workload": wl, "commit": a.commit, "source": a.dir, "kernels": out})
+    recs.append({"workload": wl, "commit": a.commit, "build_id": a.build_id, "source": a.dir, "kernels": out})
     json.dump(recs, open(a.json, "w"), indent=1)

@@ -46,6 +46,10 @@
 #include "yuma_hip.h"
 
 #define YUMA_VERSION_STRING "yuma_hip 0.1.0 gfx950"
+// the source identity the build stamps in (-DYUMA_BUILD_ID=...; yuma_build_id)
+#ifndef YUMA_BUILD_ID
+#define YUMA_BUILD_ID "unstamped"
+#endif
 
 // Kernel variants are A/B-tested from patched copies of this file
 // (tools/ab_build.py), so the product source carries no build switches.
@@ -2983,6 +2987,8 @@ struct BondArgs {
   const float* csb;   // Yuma / Yuma2: [slice][M] Σ_v S·W_b (k_rank_s), or null
   const float* csr;   // ... RN(1 / csb) or NaN (the column fails the division screen)
   const float* R;     // [slice][M] rank R = Σ_v S·Wc (YumaRust's first bond column sum)
+  const int* csrep;   // shared inputs: per scenario, the rank class representative whose
+                      // rank pass formed csb / csr (k_classes with bond_penalty), or null
   float* cpart;       // YumaRust above kRegRows validators: [N][row block][M] column partials
   int N, V, M, tiles, rowblocks, t0, t1;
   int wsh;      // every scenario reads input slice t (yuma_run_shared)
@@ -3818,8 +3824,12 @@ __global__ __launch_bounds__(BS, 1) void k_bonds_elem(BondArgs A) {
   constexpr int kQBuf = 256, NWB = BS / 64;
   __shared__ float qbuf[DPL == DP_QTE ? NWB * R * kQBuf : 1];
   int tq = A.t0;  // first epoch held in qbuf
+  // a duplicate scenario of a rank class reads its representative's column sums
+  // (the rank pass skips duplicate slices; k_incentive copies R, not csb / csr)
+  const int ncs = (COLNORM && A.csrep != nullptr) ? A.csrep[n] : n;
   auto fetch = [&](int k, int t) {
     const long long slice = (long long)t * N + n;
+    const long long cslice = (long long)t * N + ncs;
 #pragma unroll
     for (int i = 0; i < R; ++i) {
       const int rr = min(row0 + G * i, V - 1);
@@ -3841,16 +3851,16 @@ __global__ __launch_bounds__(BS, 1) void k_bonds_elem(BondArgs A) {
       if (liquid) load4c<true>(A.ba + slice * M, 0, 1, m, M, rba[k]);
       if constexpr (COLNORM) {
         load4c<true>(A.C + slice * M, 0, 1, m, M, rcc[k]);
-        load4c<true>(A.csb + slice * M, 0, 1, m, M, rcs[k]);
-        load4c<true>(A.csr + slice * M, 0, 1, m, M, rcr[k]);
+        load4c<true>(A.csb + cslice * M, 0, 1, m, M, rcs[k]);
+        load4c<true>(A.csr + cslice * M, 0, 1, m, M, rcr[k]);
       }
     } else {
       vec4raw(A.I + slice * M, m, M, ri[k]);
       if (liquid) vec4raw(A.ba + slice * M, m, M, rba[k]);
       if constexpr (COLNORM) {
         vec4raw(A.C + slice * M, m, M, rcc[k]);
-        vec4raw(A.csb + slice * M, m, M, rcs[k]);
-        vec4raw(A.csr + slice * M, m, M, rcr[k]);
+        vec4raw(A.csb + cslice * M, m, M, rcs[k]);
+        vec4raw(A.csr + cslice * M, m, M, rcr[k]);
       }
     }
   };
@@ -5393,6 +5403,7 @@ int run_impl(int variant, const yuma_params_t* prm, int N, int E, int V, int M, 
     A.rq4 = ws.rq4;
     A.csb = csb;
     A.csr = ws.csr;
+    A.csrep = csb != nullptr ? rcrep : nullptr;
     A.R = Rr;
     A.cpart = ws.cpart;
     A.N = N;
@@ -5754,5 +5765,6 @@ int yuma_graph_destroy(yuma_graph_t graph) {
 
 const char* yuma_last_error(void) { return g_err; }
 const char* yuma_version(void) { return YUMA_VERSION_STRING; }
+const char* yuma_build_id(void) { return YUMA_BUILD_ID; }
 
 }  // extern "C"

@@ -53,6 +53,7 @@ EXPORTED_SYMBOLS = (
     "yuma_graph_destroy",
     "yuma_last_error",
     "yuma_version",
+    "yuma_build_id",
 )
 
 
@@ -182,6 +183,9 @@ def load_library(path: str | None = None):
         lib.yuma_last_error.restype = ctypes.c_char_p
         lib.yuma_version.argtypes = []
         lib.yuma_version.restype = ctypes.c_char_p
+        if hasattr(lib, "yuma_build_id"):  # (A/B libraries of older sources lack it)
+            lib.yuma_build_id.argtypes = []
+            lib.yuma_build_id.restype = ctypes.c_char_p
         _lib = lib
         return lib
 
@@ -564,3 +568,11 @@ def synth_weights(seed: int, E: int, N: int, V: int, M: int, t0: int = 0,
 
 def version() -> str:
     return load_library().yuma_version().decode()
+
+
+def build_id() -> str:
+    """The library's source identity (yuma_build_id: "src-" + SHA-256 prefix of
+    the engine source and header it was built from)."""
+    lib = load_library()
+    return lib.yuma_build_id().decode() if hasattr(lib, "yuma_build_id") else "unstamped"
+
