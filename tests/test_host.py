@@ -281,13 +281,21 @@ def test_scripts_import_without_gpu():
         assert callable(importlib.import_module(name).main)
 
 
-def test_bench_line_helpers():
+def test_bench_line_helpers(monkeypatch):
     """bench.py's phase -> kernel names and committed PMC traffic lookup (the
-    pieces of the JSON line that need no GPU)."""
+    pieces of the JSON line that need no GPU). The lookup is checked as if
+    this library were the build the committed records were measured on
+    (bench pairs a record only with its own build: test below)."""
+    import json
     import sys
 
     sys.path.insert(0, ROOT)
     import bench
+
+    recs = json.load(open(bench.TRAFFIC_JSON))
+    ids = {r.get("build_id") for r in recs}
+    assert len(ids) == 1, f"the committed PMC records come from several builds: {ids}"
+    monkeypatch.setattr(bench, "engine_build_id", lambda: next(iter(ids)))
 
     for variant in range(5):
         for phase in engine.PHASES:
