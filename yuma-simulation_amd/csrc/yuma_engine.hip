@@ -3316,6 +3316,7 @@ __global__ __launch_bounds__(NT) void k_bonds(BondArgs A) {
 // strip): [slice][strip][V], k_finalize adds the strips.
 // ---------------------------------------------------------------------------
 constexpr int kCnStrip = 16;  // miners per column-normalised block
+constexpr int kCnDB = 32;     // k_bonds_cn: epochs of dividend partials parked in LDS per flush
 
 
 // Sum over the NW waves (in order) of per-wave column partials: wave w's DPP
@@ -3343,7 +3344,7 @@ __device__ __forceinline__ void cn_wave_sums(float (&x)[4], float (*red)[kCnStri
   x[3] = a.w;
 }
 
-template <int VARIANT, int R, int P, int NW = 8>
+template <int VARIANT, int R, int P, int NW = 8, bool RQ = false>
 __global__ __launch_bounds__(64 * NW, 1) void k_bonds_cn(BondArgs A) {
   constexpr bool RUST = VARIANT == YUMA_VARIANT_RUST, YUMA2 = VARIANT == YUMA_VARIANT_YUMA2;
   constexpr int RS = 16 * NW;  // row stride between a lane's rows
@@ -3420,14 +3421,16 @@ __global__ __launch_bounds__(64 * NW, 1) void k_bonds_cn(BondArgs A) {
     }
   }
 
-  // the inputs of the next P epochs in flight: W rows, row sums, stakes, and
-  // the strip's consensus, incentive and (liquid) bond_alpha; YumaRust also
-  // its rank R, which is its first bond column sum: B_sum = Σ_v S·Wc
-  // (yumas.py:113-114) is R's expression (:103), formed once by the rank pass
-  float rw[P][R][4], rd[P][R], rsn[P][R], rcc[P][4], ri[P][4], rba[P][4], rrk[P][4];
+  // the inputs of the next P epochs in flight: W rows, row sums, k_rowsum's
+  // screened RN(1 / row sum) (RQ), stakes, and the strip's consensus,
+  // incentive and (liquid) bond_alpha; YumaRust also its rank R, which is its
+  // first bond column sum: B_sum = Σ_v S·Wc (yumas.py:113-114) is R's
+  // expression (:103), formed once by the rank pass
+  float rw[P][R][4], rd[P][R], rq[P][R], rsn[P][R], rcc[P][4], ri[P][4], rba[P][4], rrk[P][4];
   auto fetch = [&](int k, int t) {
     const long long slice = (long long)t * N + n;
-    const float* Wt = A.W + (A.wsh ? (long long)t : slice) * VM;
+    const long long isl = A.wsh ? (long long)t : slice;
+    const float* Wt = A.W + isl * VM;
 #pragma unroll
     for (int i = 0; i < R; ++i) {
       const int rr_ = min(row0 + RS * i, V - 1);
@@ -3438,6 +3441,9 @@ __global__ __launch_bounds__(64 * NW, 1) void k_bonds_cn(BondArgs A) {
       rw[k][i][3] = x.w;
       rd[k][i] = A.rsd[slice * V + rr_];
       rsn[k][i] = A.sn[slice * V + rr_];
+      // the reciprocal alone (rq4.y): a 16-byte rq4 load made the compiler
+      // copy it out of the tuple right after the load (k_bonds_elem RQ)
+      if constexpr (RQ) rq[k][i] = reinterpret_cast<const float*>(A.rq4)[(isl * V + rr_) * 4 + 1];
     }
     load4c<true>(A.C + slice * M, 0, 1, m, M, rcc[k]);
     load4c<true>(A.I + slice * M, 0, 1, m, M, ri[k]);
@@ -3447,6 +3453,54 @@ __global__ __launch_bounds__(64 * NW, 1) void k_bonds_cn(BondArgs A) {
 #pragma unroll
   for (int k = 0; k < P; ++k)
     if (A.t0 + k < A.t1) fetch(k, A.t0 + k);
+
+  // RN(1 / d[c]) of the lane's four column divisors (the column sums; every
+  // lane of a column quad holds the same bits): lane c of each lane quad
+  // divides once and the quad takes the four results by DPP broadcast, one
+  // IEEE division per lane instead of four
+  const int qsel = lane & 3;
+  auto col_rcp = [&](const float (&d)[4], RowDiv (&cd)[4]) {
+    const float dm = qsel == 0 ? d[0] : qsel == 1 ? d[1] : qsel == 2 ? d[2] : d[3];
+    const float rm = 1.0f / dm;
+    const float r0 = dpp_f<0x00>(rm), r1 = dpp_f<0x55>(rm), r2 = dpp_f<0xAA>(rm), r3 = dpp_f<0xFF>(rm);
+    const float r[4] = {r0, r1, r2, r3};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const float ad = fabsf(d[c]);
+      cd[c] = {d[c], r[c], ad >= 0x1p-60f && ad <= 0x1p60f};
+    }
+  };
+
+  // Dividend partials parked per wave in LDS (DB epochs x R row sets x the
+  // wave's 16 rows) and written as 64-byte row runs when the buffer fills or
+  // the launch ends: no global store of a 4-byte partial inside the epoch loop
+  // (the history-less scan's LDS parking: c4 bonds 1.50 -> 1.41 ms)
+  constexpr int DB = R <= 2 ? kCnDB : 2 * kCnDB / R;  // 32 KiB per block
+  __shared__ __attribute__((aligned(16))) float dpark[NW * DB * R * 16];
+  float* dpb = dpark + wave * (DB * R * 16);
+  int tq = A.t0;  // first epoch held in the wave's buffer
+  auto flush_d = [&](int t) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int ne = (t - tq + 1) * R * 4;  // 16-byte pieces: (epoch, row set, row quad)
+    for (int j = lane; j < ne; j += 64) {
+      const int q4 = j & 3, i = (j >> 2) % R, e = (j >> 2) / R;
+      const int r = 16 * wave + RS * i + 4 * q4;
+      float* dst = A.dpart + (((long long)(tq + e) * N + n) * A.cblocks + strip) * V + r;
+      const float* src = dpb + j * 4;
+      if ((V & 3) == 0 && r + 3 < V) {
+        *reinterpret_cast<float4*>(dst) = *reinterpret_cast<const float4*>(src);
+      } else {
+        for (int q = 0; q < 4; ++q)
+          if (r + q < V) dst[q] = src[q];
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    tq = t + 1;
+  };
 
   int par = 0;  // LDS buffer of this epoch's first column sum
   for (int tb = A.t0; tb < A.t1; tb += P) {
@@ -3461,15 +3515,31 @@ __global__ __launch_bounds__(64 * NW, 1) void k_bonds_cn(BondArgs A) {
         bac[c] = liquid ? rba[k][c] : p_ba;
         omba[c] = liquid ? 1.0f - rba[k][c] : p_omba;
       }
-      // normalised weights (yumas.py:186), padding rows / columns zero
+      // normalised weights (yumas.py:186), padding rows / columns zero. RQ:
+      // Markstein's correction from k_rowsum's screened reciprocal (the
+      // screen covers the row's every weight: no per-element guard; a NaN
+      // sends the wave to IEEE division, the same values)
       float wn[R][4], s[R];
       {
         bool slow = false;
 #pragma unroll
         for (int i = 0; i < R; ++i) {
-          const RowDiv rdv = row_div(rd[k][i]);
+          if constexpr (RQ) {
+            const float d = rd[k][i], r = rq[k][i];
+            slow |= r != r;
 #pragma unroll
-          for (int c = 0; c < 4; ++c) wn[i][c] = div_fast(rw[k][i][c], rdv, slow);
+            for (int c = 0; c < 4; ++c) {
+              const float x = rw[k][i][c];
+              const float q = x * r;
+              const float e = fmaf(-d, q, x);
+              const float q1 = fmaf(e, r, q);
+              wn[i][c] = x == 0.0f ? q : q1;
+            }
+          } else {
+            const RowDiv rdv = row_div(rd[k][i]);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) wn[i][c] = div_fast(rw[k][i][c], rdv, slow);
+          }
         }
         if (__any(slow)) {
 #pragma unroll
@@ -3486,14 +3556,15 @@ __global__ __launch_bounds__(64 * NW, 1) void k_bonds_cn(BondArgs A) {
         for (int c = 0; c < 4; ++c) wn[i][c] = (live && colok) ? wn[i][c] : 0.0f;
       }
       // instantaneous bonds: S·W_b (Yuma, Yuma2: W_b = (1-β) W + β Wc;
-      // YumaRust: S·Wc) over their column sums
+      // YumaRust: S·Wc) over their column sums. The clip by v_minimum: C is a
+      // quantised level >= +0, so its -0 < +0 order gives torch.min's bits
       float num[R][4], csum[4] = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
       for (int i = 0; i < R; ++i)
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
           const float src = (YUMA2 && have_wp) ? Wp[i][c] : wn[i][c];
-          const float wc = tmin(src, rcc[k][c]);
+          const float wc = vmin(src, rcc[k][c]);
           const float wb = RUST ? wc : p_ompen * src + p_pen * wc;
           num[i][c] = s[i] * wb;
           csum[c] = csum[c] + num[i][c];
@@ -3510,7 +3581,7 @@ __global__ __launch_bounds__(64 * NW, 1) void k_bonds_cn(BondArgs A) {
       for (int c = 0; c < 4; ++c) ic[c] = ri[k][c];
       if constexpr (RUST) {
 #pragma unroll
-        for (int c = 0; c < 4; ++c) csum[c] = rrk[k][c];
+        for (int c = 0; c < 4; ++c) csum[c] = rrk[k][c] + 1e-6f;  // B / (B.sum(0) + 1e-6)
       }
       if (t + P < A.t1) fetch(k, t + P);  // slot k consumed: refill it
       if constexpr (!RUST) {
@@ -3520,26 +3591,27 @@ __global__ __launch_bounds__(64 * NW, 1) void k_bonds_cn(BondArgs A) {
       float ema[4] = {0.0f, 0.0f, 0.0f, 0.0f};
       {
         RowDiv cd[4];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) cd[c] = row_div(RUST ? csum[c] + 1e-6f : csum[c]);
+        col_rcp(csum, cd);
         float bi[R][4];
         bool slow = false;
 #pragma unroll
         for (int i = 0; i < R; ++i)
 #pragma unroll
           for (int c = 0; c < 4; ++c) bi[i][c] = div_fast(num[i][c], cd[c], slow);
+        // the fast path's quotients are finite (operands inside the guard):
+        // nan_to_num is the identity there
         if (__any(slow)) {
 #pragma unroll
           for (int i = 0; i < R; ++i)
 #pragma unroll
-            for (int c = 0; c < 4; ++c) bi[i][c] = num[i][c] / cd[c].d;
+            for (int c = 0; c < 4; ++c) bi[i][c] = nan_to_num(num[i][c] / cd[c].d, 0.0f);
         }
 #pragma unroll
         for (int i = 0; i < R; ++i) {
           const bool live = row0 + RS * i < V;
 #pragma unroll
           for (int c = 0; c < 4; ++c) {
-            const float b = nan_to_num(bi[i][c], 0.0f);
+            const float b = bi[i][c];
             float e = has_old ? bac[c] * b + omba[c] * B[i][c] : b;
             e = (live && colok) ? e : 0.0f;
             B[i][c] = e;
@@ -3550,9 +3622,10 @@ __global__ __launch_bounds__(64 * NW, 1) void k_bonds_cn(BondArgs A) {
       if constexpr (RUST) {  // B_ema / (Σ_v B_ema + 1e-6), nan_to_num (yumas.py:147-149)
         cn_wave_sums<NW>(ema, red[par], cq, rr, wave);
         par ^= 1;
-        RowDiv cd[4];
 #pragma unroll
-        for (int c = 0; c < 4; ++c) cd[c] = row_div(ema[c] + 1e-6f);
+        for (int c = 0; c < 4; ++c) ema[c] = ema[c] + 1e-6f;
+        RowDiv cd[4];
+        col_rcp(ema, cd);
         float q[R][4];
         bool slow = false;
 #pragma unroll
@@ -3563,12 +3636,12 @@ __global__ __launch_bounds__(64 * NW, 1) void k_bonds_cn(BondArgs A) {
 #pragma unroll
           for (int i = 0; i < R; ++i)
 #pragma unroll
-            for (int c = 0; c < 4; ++c) q[i][c] = B[i][c] / cd[c].d;
+            for (int c = 0; c < 4; ++c) q[i][c] = nan_to_num(B[i][c] / cd[c].d, 0.0f);
         }
 #pragma unroll
         for (int i = 0; i < R; ++i)
 #pragma unroll
-          for (int c = 0; c < 4; ++c) B[i][c] = nan_to_num(q[i][c], 0.0f);
+          for (int c = 0; c < 4; ++c) B[i][c] = q[i][c];
       }
       has_old = true;
       // bond history and the dividend partials Σ_{m in strip} B·I (the four
@@ -3584,8 +3657,9 @@ __global__ __launch_bounds__(64 * NW, 1) void k_bonds_cn(BondArgs A) {
         for (int c = 0; c < 4; ++c) d = d + B[i][c] * ic[c];
         d = colok ? d : 0.0f;
         d = qsum4(d);
-        if (cq == 0 && row < V) A.dpart[(slice * A.cblocks + strip) * (long long)V + row] = d;
+        if (cq == 0) dpb[((t - tq) * R + i) * 16 + rr] = d;
       }
+      if (t - tq == DB - 1 || t == A.t1 - 1) flush_d(t);  // block-uniform
     }
   }
 #pragma unroll
@@ -5079,7 +5153,10 @@ int launch_cn(hipStream_t st, yk::BondArgs& A, int* ptiles) {
   *ptiles = A.cblocks;
   const long long nblocks = (long long)A.N * A.cblocks;
   constexpr int P = NW == 8 ? (R <= 2 ? 4 : (R == 4 ? 2 : 1)) : (R <= 4 ? 3 : 2);
-  YK_LAUNCH((yk::k_bonds_cn<VARIANT, R, P, NW>), nblocks, 64 * NW, st, A);
+  if (A.rq4 != nullptr)  // k_rowsum's screened reciprocals (run_impl; not the shard stages)
+    YK_LAUNCH((yk::k_bonds_cn<VARIANT, R, P, NW, true>), nblocks, 64 * NW, st, A);
+  else
+    YK_LAUNCH((yk::k_bonds_cn<VARIANT, R, P, NW, false>), nblocks, 64 * NW, st, A);
   return yk::DP_TV;
 }
 // YumaRust's strip scan: 8 waves per 16-miner strip. Fewer waves with more
