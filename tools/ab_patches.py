@@ -328,3 +328,19 @@ PATCHES["diag_cn_nobar"] = [("        cn_wave_sums<NW>(ema, red[par], cq, rr, wa
                              "        cn_wave_sums<1>(ema, red[par], cq, rr, wave);")]
 PATCHES["diag_cn_noflush"] = [("      if (t - tq == DB - 1 || t == A.t1 - 1) flush_d(t);  // block-uniform",
                                "      if (t - tq == DB - 1 || t == A.t1 - 1) tq = t + 1;")]
+
+# k_bonds_cn ring loads without phis (round 6): bond_alpha loaded from I when
+# the scenario is not liquid (no conditional load), and the refills clamped
+# to the last epoch instead of skipped
+_CN_BA = [("    if (liquid) load4c<true>(A.ba + slice * M, 0, 1, m, M, rba[k]);\n    if (RUST) load4c<true>(A.R + slice * M, 0, 1, m, M, rrk[k]);",
+           "    load4c<true>((liquid ? A.ba : A.I) + slice * M, 0, 1, m, M, rba[k]);\n    if (RUST) load4c<true>(A.R + slice * M, 0, 1, m, M, rrk[k]);")]
+_CN_CLAMP = [("  for (int k = 0; k < P; ++k)\n    if (A.t0 + k < A.t1) fetch(k, A.t0 + k);\n\n  // RN(1 / d[c])",
+              "  for (int k = 0; k < P; ++k) fetch(k, min(A.t0 + k, A.t1 - 1));\n\n  // RN(1 / d[c])"),
+             ("      if (t + P < A.t1) fetch(k, t + P);  // slot k consumed: refill it\n      if constexpr (!RUST) {\n        cn_wave_sums<NW>(csum, red[par], cq, rr, wave);",
+              "      fetch(k, min(t + P, A.t1 - 1));  // slot k consumed: refill it\n      if constexpr (!RUST) {\n        cn_wave_sums<NW>(csum, red[par], cq, rr, wave);")]
+PATCHES["cnl_ba"] = _CN_BA
+PATCHES["cnl_clamp"] = _CN_BA + _CN_CLAMP
+_CN_P = "  constexpr int P = NW == 8 ? (R <= 2 ? 4 : (R == 4 ? 2 : 1)) : (R <= 4 ? 3 : 2);"
+PATCHES["cnl_p2"] = [(_CN_P, _CN_P.replace("(R <= 2 ? 4 :", "(R <= 2 ? 2 :"))]
+PATCHES["cnl_p3"] = [(_CN_P, _CN_P.replace("(R <= 2 ? 4 :", "(R <= 2 ? 3 :"))]
+PATCHES["cnl_clamp_p3"] = PATCHES["cnl_clamp"] + PATCHES["cnl_p3"]
