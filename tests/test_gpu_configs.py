@@ -399,3 +399,46 @@ def bench_sim(**kw):
     from yuma_simulation._internal.yumas import SimulationHyperparameters
 
     return SimulationHyperparameters(**kw)
+
+
+@pytest.mark.parametrize("case", ["negative_weight", "alpha_above_one", "state_above_one", "liquid_negative_weight"])
+def test_sweep_bounded_update_and_its_fallbacks(case):
+    """The sweep scan drops Yuma 4's two clamps when a wave's bond state starts
+    in [0, 1], every bond_alpha and 1 - bond_alpha are in [0, 1] and its rows
+    carry no negative weight (grp_scan BND, yumas.py:574-586); otherwise it
+    keeps them. Each case breaks one condition for part of the grid and must
+    still give bitwise the replicated run (k_bonds_elem, always clamped):
+    a negative weight in one row at one epoch, bond_alpha = 1.5 for some
+    scenarios, a starting bond state above 1, and the negative weight again
+    with liquid alpha on half of the grid (mixed blocks). (A liquid alpha
+    outside (0, 1) is a ValueError before any run, as in the reference.)"""
+    E, N, V, M = 9, 8, 64, 512
+    seed = 0x5EEDB0D
+    W1 = engine.synth_weights(seed, E, 1, V, M)
+    S1 = torch.from_numpy(synth.stakes(seed, E, 1, V, period=4)).to(W1.device)
+    cfgs = []
+    for i in range(N):
+        ba = 0.05 + 0.07 * i
+        if case == "alpha_above_one" and i % 3 == 1:
+            ba = 1.5
+        liq = case == "liquid_negative_weight" and i % 2 == 0
+        yp = YumaParams(bond_alpha=ba, liquid_alpha=liq)
+        cfgs.append(YumaConfig(simulation=bench_sim(kappa=0.35 + 0.1 * (i % 2)), yuma_params=yp))
+    if case in ("negative_weight", "liquid_negative_weight"):
+        W1[4, 0, 17, 100] = -3.0
+    B0 = None
+    if case == "state_above_one":
+        B0 = torch.rand(N, V, M, device=W1.device)
+        B0[:, 5, :] += 1.0
+    params = [engine.make_params(engine.VARIANT_YUMA4, c) for c in cfgs]
+    a = engine.run(engine.VARIANT_YUMA4, params, W1, S1, B0, want_hist=False, shared_inputs=True)
+    b = engine.run(engine.VARIANT_YUMA4, params, W1.expand(E, N, V, M).contiguous(), S1.expand(E, N, V).contiguous(),
+                   B0, want_hist=False)
+    torch.cuda.synchronize()
+    for k in ("C", "Dn", "I", "B_final"):
+        assert torch.equal(getattr(a, k), getattr(b, k)), f"{case}: {k} differs from the replicated run"
+    if case != "state_above_one":
+        ref = orc.run("Yuma 4 (Rhef+relative bonds)", W1[:, 0].cpu().numpy(), S1[:, 0].cpu().numpy(), cfgs[1])
+        np.testing.assert_array_equal(a.C[:, 1].cpu().numpy(), ref["C"])
+        assert_close(a.Dn[:, 1].cpu().numpy(), ref["Dn"], what=f"{case} Dn")
+        assert_close(a.B_final[1].cpu().numpy(), ref["B"][-1], what=f"{case} B_final")

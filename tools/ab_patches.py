@@ -344,3 +344,11 @@ _CN_P = "  constexpr int P = NW == 8 ? (R <= 2 ? 4 : (R == 4 ? 2 : 1)) : (R <= 4
 PATCHES["cnl_p2"] = [(_CN_P, _CN_P.replace("(R <= 2 ? 4 :", "(R <= 2 ? 2 :"))]
 PATCHES["cnl_p3"] = [(_CN_P, _CN_P.replace("(R <= 2 ? 4 :", "(R <= 2 ? 3 :"))]
 PATCHES["cnl_clamp_p3"] = PATCHES["cnl_clamp"] + PATCHES["cnl_p3"]
+
+# k_consensus_p: the pair-shared histogram's bins rotated by 32 for the column
+# groups cq >= 4 (lanes cq and cq + 4 hit the same banks at kHS = 68 words)
+PATCHES["cp_swz"] = [
+    ("          atomicAdd(hp + (col + c) * kHS + (k < w[c] ? k : w[c]), su);",
+     "          atomicAdd(hp + (col + c) * kHS + (((k < w[c] ? k : w[c]) + ((cq & 4) << 3)) & 63), su);"),
+    ("        const unsigned* hc = hp + (col + c) * kHS + 8 * rg;",
+     "        const unsigned* hc = hp + (col + c) * kHS + ((8 * rg + ((cq & 4) << 3)) & 63);")]

@@ -405,7 +405,7 @@ constexpr int kWideChunks = 64, kMaxWideChunks = 4096;
 // scan then divides without a per-row reciprocal or a per-element guard
 // (k_bonds_grp; the memory-bound scans lost with it, k_bonds_elem). k_rowsum
 // stores it per INPUT slice and row as rq4 = {row sum, this, normalised stake,
-// 0}: one 16-byte load per row and epoch.
+// 1 if some weight of the row is negative else 0}.
 __device__ __forceinline__ bool screen_ok(unsigned bmax, unsigned bmin1) {
   return bmax <= __float_as_uint(0x1p60f) && (bmin1 == 0xFFFFFFFFu || bmin1 + 1u >= __float_as_uint(0x1p-60f));
 }
@@ -430,18 +430,22 @@ __global__ __launch_bounds__(256) void k_rowsum(const float* __restrict__ W,
   const int rb = blockIdx.x % rowblocks;
   // the fast-division screen of the row (rq4): max |w| and min nonzero |w|
   // as bit patterns (|w| = 0 wraps to the maximum of bmin1)
-  unsigned bmax = 0u, bmin1 = 0xFFFFFFFFu;
+  // bneg: some weight of the row is below -0 (sign bit set, not -0; a
+  // negative-signed NaN counts), rq4.w = 1: the sweep scan's bounded Yuma 4
+  // update needs non-negative weights (k_bonds_grp)
+  unsigned bmax = 0u, bmin1 = 0xFFFFFFFFu, bneg = 0u;
   auto screen = [&](const float (&x)[4]) {
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       const unsigned b = __float_as_uint(x[c]) & 0x7FFFFFFFu;
       bmax = b > bmax ? b : bmax;
       bmin1 = b - 1u < bmin1 ? b - 1u : bmin1;
+      bneg |= __float_as_uint(x[c]) > 0x80000000u ? 1u : 0u;
     }
   };
   if constexpr (WIDE) {
     __shared__ float qs[kMaxWideChunks];
-    __shared__ unsigned qb[2][4];
+    __shared__ unsigned qb[3][4];
     const int nc = (M + 255) / 256;
     const float* r = W + (wsl * V + rb) * (long long)M;
 #pragma unroll 4
@@ -469,10 +473,12 @@ __global__ __launch_bounds__(256) void k_rowsum(const float* __restrict__ W,
     for (int o = 1; o < 64; o <<= 1) {
       bmax = max(bmax, (unsigned)__shfl_xor((int)bmax, o, 64));
       bmin1 = min(bmin1, (unsigned)__shfl_xor((int)bmin1, o, 64));
+      bneg |= (unsigned)__shfl_xor((int)bneg, o, 64);
     }
     if (lane == 0) {
       qb[0][wave] = bmax;
       qb[1][wave] = bmin1;
+      qb[2][wave] = bneg;
     }
     __syncthreads();
     if (wave == 0) {
@@ -483,12 +489,14 @@ __global__ __launch_bounds__(256) void k_rowsum(const float* __restrict__ W,
       const float rs = partial ? acc : acc + 1e-6f;
       for (int f = lane; f < fan; f += 64) rsd[(wsl * fan + f) * V + rb] = rs;
       if (rq4 != nullptr && lane == 0) {
-        unsigned bx = qb[0][0], bn = qb[1][0];
+        unsigned bx = qb[0][0], bn = qb[1][0], ng = qb[2][0];
         for (int w = 1; w < 4; ++w) {
           bx = max(bx, qb[0][w]);
           bn = min(bn, qb[1][w]);
+          ng |= qb[2][w];
         }
         *reinterpret_cast<float2*>(&rq4[wsl * V + rb]) = make_float2(rs, fast_row_rcp(rs, bx, bn));
+        reinterpret_cast<float*>(&rq4[wsl * V + rb])[3] = ng ? 1.0f : 0.0f;
       }
     }
   }
@@ -526,9 +534,12 @@ __global__ __launch_bounds__(256) void k_rowsum(const float* __restrict__ W,
       for (int o = 1; o < 64; o <<= 1) {
         bmax = max(bmax, (unsigned)__shfl_xor((int)bmax, o, 64));
         bmin1 = min(bmin1, (unsigned)__shfl_xor((int)bmin1, o, 64));
+        bneg |= (unsigned)__shfl_xor((int)bneg, o, 64);
       }
-      if (lane == 0)
+      if (lane == 0) {
         *reinterpret_cast<float2*>(&rq4[wsl * V + row]) = make_float2(rs, fast_row_rcp(rs, bmax, bmin1));
+        reinterpret_cast<float*>(&rq4[wsl * V + row])[3] = bneg ? 1.0f : 0.0f;
+      }
     }
   }
   // the stake normalisation: output slices f = rb, rb + rowblocks, ... of
@@ -4178,7 +4189,16 @@ constexpr bool kGrpPark = true;  // dividend partials parked per wave in LDS
 constexpr int kGrpDB = 32;       // ... epochs per flush
 // LQ: 0 = every scenario of the block has a fixed bond_alpha (block-uniform
 // operands), 2 = every one is liquid (per-miner bond_alpha), 1 = mixed.
-template <int VARIANT, int K, int R, int P, int LQ, bool HIST>
+// BND (Yuma 4): the wave's bond state starts in [0, 1] (or NaN), every
+// scenario's bond_alpha and 1 - bond_alpha lie in [0, 1] and no weight of the
+// wave's rows is negative over the launch (k_bonds_grp decides it per wave).
+// Then Bd = B (1 - a) is in [0, 1], so 1 - Bd >= +0 and the clamp(min = 0)
+// of the remaining capacity is the identity; and Bd + min(a W, RN(1 - Bd))
+// rounds to at most 1 (1 - Bd is exact for Bd >= 1/2, otherwise within
+// 2^-25 of it, below the half-ulp of 1 above 1), so the clamp(max = 1) is the
+// identity too and B stays in [0, 1]: the update drops both clamps with the
+// same bits (yumas.py:574-586). NaN operands propagate alike in both forms.
+template <int VARIANT, int K, int R, int P, int LQ, bool HIST, bool BND = false>
 __device__ __forceinline__ void grp_scan(const BondArgs& A, unsigned liquid_mask, float* dpark) {
   constexpr bool LIQ = LQ != 0;
   constexpr int G = 16;
@@ -4446,6 +4466,12 @@ __device__ __forceinline__ void grp_scan(const BondArgs& A, unsigned liquid_mask
               const float nb = p_dk[k] * B[k][i][c] + pc * wn[i][c];
               B[k][i][c] = tmin(nb, cap);
             }
+          } else if (BND) {
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+              const float bd = B[k][i][c] * omba[c];
+              B[k][i][c] = bd + vmin(bac[c] * wn[i][c], 1.0f - bd);
+            }
           } else {
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
@@ -4506,6 +4532,56 @@ __global__ __launch_bounds__(256, kGrpWaves) void k_bonds_grp(BondArgs A) {
   for (int k = 0; k < K; ++k)
     if (n0 + k < A.N && A.prm[n0 + k].liquid_mode != YUMA_LIQUID_OFF) liquid_mask |= 1u << k;
   const int nk = A.N - n0 < K ? A.N - n0 : K;
+  if constexpr (VARIANT == YUMA_VARIANT_YUMA4) {
+    // the bounded update (grp_scan BND), decided per wave (the scan has no
+    // block barrier): parameters, the wave's starting bond state and its
+    // rows' weights over the launch (k_rowsum's negative-weight flag rq4.w)
+    bool ok = A.rq4 != nullptr;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      if (k >= nk) break;
+      const yuma_params_t& pg = A.prm[n0 + k];
+      if ((liquid_mask >> k) & 1u)  // bond_alpha = 1 - clamp(alpha, alpha_low, alpha_high)
+        ok = ok && pg.alpha_low >= 0.0f && pg.alpha_low <= 1.0f && pg.alpha_high >= 0.0f && pg.alpha_high <= 1.0f;
+      else
+        ok = ok && pg.bond_alpha >= 0.0f && pg.bond_alpha <= 1.0f && pg.one_minus_bond_alpha >= 0.0f &&
+             pg.one_minus_bond_alpha <= 1.0f;
+    }
+    const Lay L = lay();
+    const int tile = blockIdx.x % A.tiles, rb = (blockIdx.x / A.tiles) % A.rowblocks;
+    const int m = tile * kTileM + L.c4 * 4, row0 = rb * 16 * R + L.g;
+    const float* src = A.t0 == 0 ? A.B_init : A.Bstate;
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const int row = row0 + 16 * i;
+      if (row >= A.V) continue;
+      if (src != nullptr && m < A.M)
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          if (k >= nk) break;
+          float b[4];
+          load4<true>(src + (long long)(n0 + k) * A.V * A.M + (long long)row * A.M, m, A.M, b);
+#pragma unroll
+          for (int c = 0; c < 4; ++c) ok &= (b[c] >= 0.0f && b[c] <= 1.0f) || b[c] != b[c];
+        }
+      if (A.rq4 != nullptr) {  // independent loads (no short-circuit chain of load latencies)
+        float neg = 0.0f;
+        const float* fw = reinterpret_cast<const float*>(A.rq4 + (long long)A.t0 * A.V + row) + 3;
+#pragma unroll 8
+        for (int t = A.t0; t < A.t1; ++t, fw += 4 * A.V) neg = fmaxf(neg, *fw);
+        ok &= neg == 0.0f;
+      }
+    }
+    if (__all(ok)) {
+      if (liquid_mask == (1u << nk) - 1u)
+        grp_scan<VARIANT, K, R, P, 2, HIST, true>(A, liquid_mask, dpark);
+      else if (liquid_mask != 0)
+        grp_scan<VARIANT, K, R, P, 1, HIST, true>(A, liquid_mask, dpark);
+      else
+        grp_scan<VARIANT, K, R, P, 0, HIST, true>(A, 0u, dpark);
+      return;
+    }
+  }
   if (VARIANT == YUMA_VARIANT_YUMA4 && liquid_mask == (1u << nk) - 1u)  // block-uniform; Yuma3 has no bond_alpha
     grp_scan<VARIANT, K, R, P, 2, HIST>(A, liquid_mask, dpark);
   else if (VARIANT == YUMA_VARIANT_YUMA4 && liquid_mask != 0)
