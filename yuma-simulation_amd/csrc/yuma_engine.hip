@@ -204,6 +204,30 @@ __global__ __launch_bounds__(256) void k_classes(const yuma_params_t* __restrict
     crep[n] = r;
   }
 }
+// The representatives of k_classes' classes in scenario order, compacted:
+// clist[0] = the class count, clist[1 + j] = the j-th representative (one
+// block; the multi-class consensus of a sweep walks this list)
+__global__ __launch_bounds__(256) void k_class_list(const int* __restrict__ crep, int N, int* __restrict__ clist) {
+  __shared__ int wc[4];
+  __shared__ int base;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (threadIdx.x == 0) base = 0;
+  __syncthreads();
+  for (int n0 = 0; n0 < N; n0 += 256) {
+    const int n = n0 + (int)threadIdx.x;
+    const bool rep = n < N && crep[n] == n;
+    const unsigned long long b = __ballot(rep);
+    if (lane == 0) wc[wave] = __popcll(b);
+    __syncthreads();
+    int off = base;
+    for (int w = 0; w < wave; ++w) off += wc[w];
+    if (rep) clist[1 + off + __popcll(b & ((1ull << lane) - 1ull))] = n;
+    __syncthreads();
+    if (threadIdx.x == 0) base += wc[0] + wc[1] + wc[2] + wc[3];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) clist[0] = base;
+}
 // is slice (t, n) computed by another scenario's block (crep[n] != n)?
 __device__ __forceinline__ bool dup_slice(const int* crep, long long slice, int N) {
   if (crep == nullptr) return false;
@@ -1460,6 +1484,56 @@ __global__ __launch_bounds__(256, 4) void k_consensus_w(const float* __restrict_
       if (m + c < M) craw[slice * M + m + c] = (double)hi_k[c] / (double)top;
 }
 
+// Shared-input sweeps (c3): every consensus class of an epoch searches the
+// same normalised tile, so a block loads and divides the epoch's 64-miner
+// tile once and runs the search of classes g, g + G, ... of the compacted
+// class list (k_class_list) on it -- the same search, the same bits as
+// k_consensus_w's per-slice blocks. Grid: epochs x tiles x G. (k_consensus_w
+// launches a block for every (slice, tile) and lets the duplicate scenarios'
+// blocks exit: at c3 31 of 32 of its 1M blocks, each class re-reading the
+// tile from the caches.)
+template <int R, bool VEC>
+__global__ __launch_bounds__(256, 4) void k_consensus_mc(const float* __restrict__ W,
+                                                      const float* __restrict__ rsd,
+                                                      const float* __restrict__ sn,
+                                                      const int* __restrict__ sx,
+                                                      const yuma_params_t* __restrict__ prm, int N,
+                                                      int V, int M, long long t0, int tiles,
+                                                      double* __restrict__ craw,
+                                                      const int* __restrict__ clist, int G) {
+  __shared__ __attribute__((aligned(16))) unsigned hb[kHistWords];
+  const WLay L = wlay();
+  const int tile = blockIdx.x % tiles;
+  const int g = (blockIdx.x / tiles) % G;
+  const long long t = t0 + blockIdx.x / (tiles * G);
+  const int nc = clist[0];
+  if (g >= nc) return;  // block-uniform
+  const int m = tile * kTileM + L.wave * 16 + L.cq * 4;
+  if (tile * kTileM + L.wave * 16 >= M) return;  // whole wave past the last miner
+  // the epoch's row sums and stakes: stored for every scenario (k_rowsum fan)
+  const long long s0 = t * N + clist[1 + g];
+  __shared__ __attribute__((aligned(16))) float rl[4][48 * R];
+  float wn[R][4];
+  load_norm_w_lds<R, VEC>(W + t * (long long)V * M, rsd + s0 * V, sn + s0 * V, rl[L.wave], V, M, m, L.rg,
+                          L.lane, wn);
+  const LdsRows s{&rl[0][0], L.wave * 48 * R + 16 * R + L.rg};
+  for (int j = g; j < nc; j += G) {
+    const int n = clist[1 + j];
+    const long long slice = t * N + n;
+    const yuma_params_t& p = prm[n];
+    const bool hist_ok = !(p.flags & YUMA_FLAG_NO_HIST);
+    int hi_k[4];
+    consensus_search<R, 16>(wn, s, p.kappa, p.bisect_iters, hist_ok ? sx[slice] : -1,
+                            hb + L.wave * 16 * kHS, L.lane, L.cq, L.rg, hi_k);
+    const int top = 1 << p.bisect_iters;
+    if (L.rg == 0)
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        if (m + c < M) craw[slice * M + m + c] = (double)hi_k[c] / (double)top;
+  }
+}
+constexpr int kMcGroups = 4;  // k_consensus_mc: blocks per (epoch, tile), each a quarter of the classes
+
 // ---------------------------------------------------------------------------
 // Consensus with 128-byte row segments (round 4). Same
 // block / tile as k_consensus_w (one 64-miner tile of one slice), but two
@@ -2042,6 +2116,117 @@ __global__ __launch_bounds__(256) void k_rank_w(
 // |S·W_b| of the column in [2^-60, 2^60], as RowDiv's guard), else NaN: the
 // scan then divides by Markstein's correction with no per-element guard, and
 // its quotients are finite, so nan_to_num is the identity there.
+// Shared-input sweeps (c3): the rank of every consensus class of an epoch
+// from one block per (epoch, tile, class group) -- k_class_list's classes g,
+// g + G, ... in chunks of KC, each chunk one walk over the tile's rows (the
+// normalised rows are formed once per walk for KC classes' clips) -- the same
+// operations and orders as k_rank_s (Yuma 3 / 4: no bond column sums), so the
+// same bits. k_rank_s launches a block for every (slice, tile) and lets the
+// duplicate scenarios' blocks exit.
+template <bool VEC, int KC>
+__global__ __launch_bounds__(256, 1) void k_rank_mc(const float* __restrict__ W,
+                                                 const float* __restrict__ rsd,
+                                                 const float* __restrict__ sn,
+                                                 const float* __restrict__ C, int N, int V, int M,
+                                                 long long t0, int tiles,
+                                                 float* __restrict__ Rout,
+                                                 float* __restrict__ rpart,
+                                                 const int* __restrict__ clist, int G) {
+  __shared__ float4 red[KC][4][16];
+  const Lay L = lay();
+  const int tile = blockIdx.x % tiles;
+  const int g = (blockIdx.x / tiles) % G;
+  const long long t = t0 + blockIdx.x / (tiles * G);
+  const int nc = clist[0];
+  if (g >= nc) return;  // block-uniform
+  const long long VM = (long long)V * M;
+  const int m = tile * kTileM + L.c4 * 4;
+  const float* Ws = W + t * VM;
+  const long long s0 = t * N + clist[1 + g];  // the epoch's row sums and stakes (every scenario's)
+  __shared__ float rows_d[kRegRows], rows_r[kRegRows], rows_s[kRegRows];
+  for (int j = threadIdx.x; j < V; j += 256) {
+    const float dj = rsd[s0 * V + j];
+    rows_d[j] = dj;
+    rows_r[j] = 1.0f / dj;
+    rows_s[j] = sn[s0 * V + j];
+  }
+  __syncthreads();
+  for (int j0 = g; j0 < nc; j0 += G * KC) {
+    float Cc[KC][4], acc[KC][4];
+    long long sl[KC];
+#pragma unroll
+    for (int q = 0; q < KC; ++q) {
+      const int j = j0 + G * q;
+      sl[q] = t * N + clist[1 + (j < nc ? j : g)];
+      load4c<VEC>(C + sl[q] * M, 0, 1, m, M, Cc[q]);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) acc[q][c] = 0.0f;
+    }
+    constexpr int B = 8;
+    for (int r0 = L.g; r0 < V; r0 += 16 * B) {
+      float w[B][4], d[B], s[B];
+#pragma unroll
+      for (int i = 0; i < B; ++i) {
+        const int rr = min(r0 + 16 * i, V - 1);
+        load4c<VEC>(Ws, rr, V, m, M, w[i]);
+        d[i] = rows_d[rr];
+        s[i] = rows_s[rr];
+      }
+      bool slow = false;
+#pragma unroll
+      for (int i = 0; i < B; ++i) {
+        const int rr = min(r0 + 16 * i, V - 1);
+        const float ad = fabsf(d[i]);
+        const RowDiv rdv{d[i], rows_r[rr], ad >= 0x1p-60f && ad <= 0x1p60f};
+#pragma unroll
+        for (int c = 0; c < 4; ++c) w[i][c] = div_fast_nz(w[i][c], rdv, slow);
+      }
+      if (__any(slow)) {  // rare: redo the batch with IEEE division (wave-uniform)
+#pragma unroll
+        for (int i = 0; i < B; ++i) {
+          const int rr = min(r0 + 16 * i, V - 1);
+          float x[4];
+          load4c<VEC>(Ws, rr, V, m, M, x);
+#pragma unroll
+          for (int c = 0; c < 4; ++c) w[i][c] = x[c] / d[i];
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < B; ++i) {
+        const bool live = r0 + 16 * i < V;
+#pragma unroll
+        for (int q = 0; q < KC; ++q)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            const float x = s[i] * vmin(w[i][c], Cc[q][c]);
+            acc[q][c] = live ? acc[q][c] + x : acc[q][c];
+          }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < KC; ++q) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) acc[q][c] = sum_rowgroups(acc[q][c]);
+      if (L.lane < 16) red[q][L.wave][L.c4] = make_float4(acc[q][0], acc[q][1], acc[q][2], acc[q][3]);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < KC; ++q) {
+      if (L.wave != q % 4 || j0 + G * q >= nc) continue;  // wave q % 4 writes class q
+      const float* rf = reinterpret_cast<const float*>(&red[q][0][0]);
+      float r = rf[L.lane];
+#pragma unroll
+      for (int w = 1; w < 4; ++w) r = r + rf[w * 64 + L.lane];
+      const int mg = tile * kTileM + L.lane;
+      if (mg < M) Rout[sl[q] * M + mg] = r;
+      float tt = mg < M ? r : 0.0f;
+      tt = wave_sum(tt);
+      if (L.lane == 0) rpart[sl[q] * tiles + tile] = tt;
+    }
+    __syncthreads();  // red[] reuse
+  }
+}
+
 template <bool VEC, bool YUMA2 = false, bool BCS = false>
 __global__ __launch_bounds__(256, 1) void k_rank_s(const float* __restrict__ W,
                                                 const float* __restrict__ rsd,
@@ -4952,6 +5137,7 @@ struct Workspace {
   float* sumc_f;
   double* sumc_d;
   int* crep;  // per scenario: consensus class representative (k_classes)
+  int* clist;  // [1 + N]: class count, then the representatives (k_class_list)
   int* rcrep;  // per scenario: rank class representative (Yuma: + bond_penalty)
   float* csb;  // Yuma / Yuma2: [slice][M] Σ_v S·W_b (k_rank_s)
   float* csr;  // ... and RN(1 / csb) where the column passes the division screen, else NaN
@@ -5000,6 +5186,7 @@ Workspace carve(char* base, int variant, int N, int E, int V, int M, int full) {
   w.sumc_f = (float*)take(S * 4);
   w.sumc_d = (double*)take(S * 8);
   w.crep = (int*)take((size_t)N * 4);
+  w.clist = (int*)take((size_t)(N + 1) * 4);
   w.rcrep = (int*)take((size_t)N * 4);
   const bool cn = variant == YUMA_VARIANT_YUMA1 || variant == YUMA_VARIANT_YUMA2;
   w.csb = cn ? (float*)take(S * M * 4) : nullptr;
@@ -5041,6 +5228,26 @@ void launch_consensus_w(long long nblocks, hipStream_t st, const float* W, const
                         const int* crep) {
   YK_LAUNCH((yk::k_consensus_w<R, VEC>), nblocks, 256, st, W, rsd, sn, sx, prm, N, V, M, slice0,
             tiles, craw, P, wsh, crep);
+}
+
+template <bool VEC>
+void launch_consensus_mc(RowCfg rc, long long nblocks, hipStream_t st, const float* W, const float* rsd,
+                         const float* sn, const int* sx, const yuma_params_t* prm, int N, int V, int M,
+                         long long t0, int tiles, double* craw, const int* clist, int G) {
+  switch (rc) {
+    case RC_256_1:
+      YK_LAUNCH((yk::k_consensus_mc<1, VEC>), nblocks, 256, st, W, rsd, sn, sx, prm, N, V, M, t0, tiles, craw,
+                clist, G);
+      return;
+    case RC_256_4:
+      YK_LAUNCH((yk::k_consensus_mc<4, VEC>), nblocks, 256, st, W, rsd, sn, sx, prm, N, V, M, t0, tiles, craw,
+                clist, G);
+      return;
+    default:
+      YK_LAUNCH((yk::k_consensus_mc<16, VEC>), nblocks, 256, st, W, rsd, sn, sx, prm, N, V, M, t0, tiles, craw,
+                clist, G);
+      return;
+  }
 }
 
 template <bool VEC>
@@ -5113,7 +5320,8 @@ void launch_rank(RowCfg rc, long long nblocks, hipStream_t st, const float* W, c
                  const float* sn, const float* C, const float* Wprev_init, int yuma2, int N,
                  int V, int M, long long slice0, int tiles, float* R, float* rpart, float* Wn,
                  float* Wc, float* tvc, float* tvn, int wsh, const int* crep = nullptr,
-                 float* csb = nullptr, float* csr = nullptr, const yuma_params_t* prm = nullptr) {
+                 float* csb = nullptr, float* csr = nullptr, const yuma_params_t* prm = nullptr,
+                 const int* clist = nullptr) {
   const bool full = Wn != nullptr || Wc != nullptr || tvc != nullptr;
   if (V > yk::kRegRows) {  // streamed rows: the wide rank with per-row loads, plus the full outputs
     const long long nb = nblocks / tiles * ((M + 255) / 256);
@@ -5156,6 +5364,12 @@ void launch_rank(RowCfg rc, long long nblocks, hipStream_t st, const float* W, c
     else
       YK_LAUNCH((yk::k_rank_sw<VEC, false>), nb, 256, st, W, rsd, sn, C, N, V, M, slice0, tiles, R,
                 rpart, wsh, crep, nullptr, nullptr, nullptr, prm);
+    return;
+  }
+  if (!full && clist != nullptr && !yuma2 && !csb) {  // shared-input sweep: every class per block
+    const int G = N < yk::kMcGroups ? N : yk::kMcGroups;
+    YK_LAUNCH((yk::k_rank_mc<VEC, 4>), nblocks / N * G, 256, st, W, rsd, sn, C, N, V, M, slice0 / N, tiles, R,
+              rpart, clist, G);
     return;
   }
   if (!full) {  // streaming rank; k_rank_w also materialises Wn / Wc / T_v
@@ -5470,6 +5684,10 @@ int run_impl(int variant, const yuma_params_t* prm, int N, int E, int V, int M, 
     YK_LAUNCH(yk::k_classes, ncb, 256, st, prm, N, ws.crep, 0);
     crep = ws.crep;
   }
+  // ... and one block per (epoch, tile, class group) searching every class on
+  // one load of the tile (k_consensus_mc; wave-owned columns, <= 256 validators)
+  const bool mc = crep != nullptr && V <= 256;
+  if (mc) YK_LAUNCH(yk::k_class_list, 1, 256, st, ws.crep, N, ws.clist);
   // Yuma / Yuma2 run outputs above 64 validators: the streaming rank also
   // forms the bond column sums Σ_v S·W_b and the bond scan is element-wise
   const bool streaming = out->Wn == nullptr && out->Wc == nullptr && ws.tvc == nullptr;
@@ -5514,7 +5732,16 @@ int run_impl(int variant, const yuma_params_t* prm, int N, int E, int V, int M, 
         YK_LAUNCH(yk::k_rowsum<false>, rs_in * rowblocks4, 256, st, W, S, V, M, rs_s0,
                   rowblocks4, ws.rsd, ws.sn, 0, ws.sx, fan, ws.rq4);
       tm.mark(YUMA_PHASE_CONSENSUS);
-      if (vec)
+      if (mc) {
+        const int G = N < yk::kMcGroups ? N : yk::kMcGroups;
+        const long long nb = (long long)(c1 - c0) * tiles * G;
+        if (vec)
+          launch_consensus_mc<true>(rc, nb, st, W, ws.rsd, ws.sn, ws.sx, prm, N, V, M, c0, tiles, ws.craw,
+                                    ws.clist, G);
+        else
+          launch_consensus_mc<false>(rc, nb, st, W, ws.rsd, ws.sn, ws.sx, prm, N, V, M, c0, tiles, ws.craw,
+                                     ws.clist, G);
+      } else if (vec)
         launch_consensus<true>(rc, ns * tiles, st, W, ws.rsd, ws.sn, ws.sx, prm, N, V, M, s0, tiles,
                                ws.craw, out->P, wsh, crep, ws.rq4);
       else
@@ -5524,14 +5751,18 @@ int run_impl(int variant, const yuma_params_t* prm, int N, int E, int V, int M, 
       YK_LAUNCH(yk::k_quantise<256>, ns, 256, st, ws.craw, prm, variant, N, M, s0, C, ws.qlev,
                 ba_buf, ws.scal, nullptr, nullptr, 0, crep);
       tm.mark(YUMA_PHASE_RANK);
+      // the multi-class rank walks the consensus classes' list: only when the
+      // rank classes are those classes (no bond column sums) and the streaming
+      // rank of <= 1024 validators on 64-miner tiles would run
+      const int* rlist = (mc && rcrep == crep && csb == nullptr && M < 16384) ? ws.clist : nullptr;
       if (vec)
         launch_rank<true>(rc, ns * tiles, st, W, ws.rsd, ws.sn, C, Wprev_init,
                           variant == YUMA_VARIANT_YUMA2, N, V, M, s0, tiles, Rr, ws.rpart, out->Wn,
-                          out->Wc, ws.tvc, ws.tvn, wsh, rcrep, csb, ws.csr, prm);
+                          out->Wc, ws.tvc, ws.tvn, wsh, rcrep, csb, ws.csr, prm, rlist);
       else
         launch_rank<false>(rc, ns * tiles, st, W, ws.rsd, ws.sn, C, Wprev_init,
                            variant == YUMA_VARIANT_YUMA2, N, V, M, s0, tiles, Rr, ws.rpart,
-                           out->Wn, out->Wc, ws.tvc, ws.tvn, wsh, rcrep, csb, ws.csr, prm);
+                           out->Wn, out->Wc, ws.tvc, ws.tvn, wsh, rcrep, csb, ws.csr, prm, rlist);
     }
     tm.mark(YUMA_PHASE_INCENTIVE);
     const int ich = (M + yk::kIncCols - 1) / yk::kIncCols;
