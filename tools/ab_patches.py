@@ -352,3 +352,16 @@ PATCHES["cp_swz"] = [
      "          atomicAdd(hp + (col + c) * kHS + (((k < w[c] ? k : w[c]) + ((cq & 4) << 3)) & 63), su);"),
     ("        const unsigned* hc = hp + (col + c) * kHS + 8 * rg;",
      "        const unsigned* hc = hp + (col + c) * kHS + ((8 * rg + ((cq & 4) << 3)) & 63);")]
+
+# k_bonds_cn: the bond history through plain (write-back) stores instead of
+# non-temporal ones, so an XCD's L2 can merge the two 64-byte halves of a
+# line written by the paired strips (PMC: 1.26x write amplification)
+PATCHES["cn_plainst"] = [(
+    "          __builtin_nontemporal_store(fvec4{B[i][0], B[i][1], B[i][2], B[i][3]},\n"
+    "                                      reinterpret_cast<fvec4*>(A.B_hist + slice * VM + (long long)row * M + m));\n"
+    "        float d = 0.0f;\n#pragma unroll\n        for (int c = 0; c < 4; ++c) d = d + B[i][c] * ic[c];\n"
+    "        d = colok ? d : 0.0f;\n        d = qsum4(d);\n        if (cq == 0) dpb[",
+    "          *reinterpret_cast<fvec4*>(A.B_hist + slice * VM + (long long)row * M + m) =\n"
+    "              fvec4{B[i][0], B[i][1], B[i][2], B[i][3]};\n"
+    "        float d = 0.0f;\n#pragma unroll\n        for (int c = 0; c < 4; ++c) d = d + B[i][c] * ic[c];\n"
+    "        d = colok ? d : 0.0f;\n        d = qsum4(d);\n        if (cq == 0) dpb[")]

@@ -3097,7 +3097,7 @@ __global__ __launch_bounds__(256) void k_incentive(float* __restrict__ Rio,
                                                    float* __restrict__ scal,
                                                    const float* __restrict__ ext_rsum,
                                                    const int* __restrict__ crep, int N,
-                                                   int nchunk, int v4) {
+                                                   int nchunk, int v4, int copyr) {
   // block = (slice, chunk of kIncCols miners): every block of a slice forms
   // the same ΣR (same order, same bits), then scales its own chunk
   constexpr int kStage = 4096;
@@ -3105,8 +3105,10 @@ __global__ __launch_bounds__(256) void k_incentive(float* __restrict__ Rio,
   __shared__ float rp[kStage];
   const long long slice = slice0 + blockIdx.x / nchunk;
   const int ch = blockIdx.x % nchunk;
-  // rank computed by the class representative (crep): R copied into this slice
+  // rank computed by the class representative (crep): R copied into this
+  // slice when someone reads it (the caller's R output; YumaRust's bond scan)
   const long long rs = rep_slice(crep, slice, N);
+  const bool cp = copyr && rs != slice;
   float s = 0.0f;
   if (ext_rsum != nullptr) {  // miner-column shard: sum over every shard
     s = ext_rsum[slice];
@@ -3135,7 +3137,7 @@ __global__ __launch_bounds__(256) void k_incentive(float* __restrict__ Rio,
     float4* i4 = reinterpret_cast<float4*>(I + slice * M);
     for (int j = ch * (kIncCols / 4) + threadIdx.x; j < m1 / 4; j += 256) {
       const float4 r = r4[j];
-      if (rs != slice) d4[j] = r;
+      if (cp) d4[j] = r;
       i4[j] = make_float4(nan_to_num(r.x / sr, 0.0f), nan_to_num(r.y / sr, 0.0f),
                           nan_to_num(r.z / sr, 0.0f), nan_to_num(r.w / sr, 0.0f));
       if (T != nullptr) {
@@ -3149,7 +3151,7 @@ __global__ __launch_bounds__(256) void k_incentive(float* __restrict__ Rio,
   }
   for (int m = ch * kIncCols + threadIdx.x; m < m1; m += 256) {
     const float r = Rio[rs * M + m];
-    if (rs != slice) Rio[slice * M + m] = r;
+    if (cp) Rio[slice * M + m] = r;
     I[slice * M + m] = nan_to_num(r / sr, 0.0f);
     if (T != nullptr) T[slice * M + m] = nan_to_num(r / Pin[slice * M + m], 0.0f);
   }
@@ -3846,8 +3848,11 @@ __global__ __launch_bounds__(64 * NW, 1) void k_bonds_cn(BondArgs A) {
       for (int i = 0; i < R; ++i) {
         const int row = row0 + RS * i;
         if (A.B_hist != nullptr && row < V && colok)
-          __builtin_nontemporal_store(fvec4{B[i][0], B[i][1], B[i][2], B[i][3]},
-                                      reinterpret_cast<fvec4*>(A.B_hist + slice * VM + (long long)row * M + m));
+          // plain (write-back) stores: the L2 of the XCD merges the paired
+          // strips' 64-byte halves of each line (non-temporal stores wrote
+          // 1.26x the history: PMC 5.65 -> 4.46 GB per c2 launch, same time)
+          *reinterpret_cast<fvec4*>(A.B_hist + slice * VM + (long long)row * M + m) =
+              fvec4{B[i][0], B[i][1], B[i][2], B[i][3]};
         float d = 0.0f;
 #pragma unroll
         for (int c = 0; c < 4; ++c) d = d + B[i][c] * ic[c];
@@ -5767,7 +5772,8 @@ int run_impl(int variant, const yuma_params_t* prm, int N, int E, int V, int M, 
     tm.mark(YUMA_PHASE_INCENTIVE);
     const int ich = (M + yk::kIncCols - 1) / yk::kIncCols;
     YK_LAUNCH(yk::k_incentive, ns * ich, 256, st, Rr, ws.rpart, out->P, M, s0, tiles, I,
-              out->P ? out->T : nullptr, ws.scal, nullptr, rcrep, N, ich, incentive_v4(M, Rr, I, out));
+              out->P ? out->T : nullptr, ws.scal, nullptr, rcrep, N, ich, incentive_v4(M, Rr, I, out),
+              (out->R != nullptr || variant == YUMA_VARIANT_RUST) ? 1 : 0);
 
     yk::BondArgs A{};
     A.W = W;
@@ -5949,7 +5955,7 @@ int shard_stage_impl(int stage, int variant, const yuma_params_t* prm, int N, in
                 rust ? 1 : 0);
       const int ich = (M + yk::kIncCols - 1) / yk::kIncCols;
       YK_LAUNCH(yk::k_incentive, ns * ich, 256, st, R, ws.rpart, out->P, M, 0LL, tiles, I,
-                out->P ? out->T : nullptr, ws.scal, io->rsum, nullptr, N, ich, incentive_v4(M, R, I, out));
+                out->P ? out->T : nullptr, ws.scal, io->rsum, nullptr, N, ich, incentive_v4(M, R, I, out), 1);
       yk::BondArgs A{};
       A.W = W;
       A.rsd = ws.rsd;
