@@ -420,3 +420,24 @@ def test_bench_ignores_counter_records_of_another_build(tmp_path, monkeypatch):
     assert bench.load_traffic(key) is None
     monkeypatch.setattr(bench, "engine_build_id", lambda: "src-0000000000000000")
     assert bench.load_traffic(key) == {"k_bonds_elem": 1.0}
+
+
+def test_committed_counter_records_are_this_build():
+    """Every committed PMC / SQ record that bench.py pairs with its timings was
+    measured on the library this tree builds: an engine
+    change without a fresh profiling pass fails here instead of pairing stale
+    counters with new kernels (bench.py would print null for them)."""
+    import json
+    import sys
+
+    import __graft_entry__ as g
+
+    sys.path.insert(0, ROOT)
+    import bench
+
+    bid = g.source_build_id()
+    for path in (bench.TRAFFIC_JSON, bench.SQ_JSON):
+        recs = json.load(open(path))
+        assert recs, path
+        for r in recs:
+            assert r.get("build_id") == bid, f"{os.path.relpath(path, ROOT)} {r['workload']}: {r.get('build_id')} != {bid}"
