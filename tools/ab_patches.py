@@ -365,3 +365,11 @@ PATCHES["cn_plainst"] = [(
     "              fvec4{B[i][0], B[i][1], B[i][2], B[i][3]};\n"
     "        float d = 0.0f;\n#pragma unroll\n        for (int c = 0; c < 4; ++c) d = d + B[i][c] * ic[c];\n"
     "        d = colok ? d : 0.0f;\n        d = qsum4(d);\n        if (cq == 0) dpb[")]
+
+# k_bonds_cn at 129-256 validators with 16 waves per strip (one row per lane)
+# on the lean arithmetic (round 4 lost this form with the heavier epoch)
+PATCHES["cn_w16"] = [("  if (V <= 256) return launch_cn<VARIANT, 2>(st, A, ptiles);",
+                      "  if (V <= 256) return launch_cn<VARIANT, 1, 16>(st, A, ptiles);")]
+PATCHES["cn_w16_p2"] = PATCHES["cn_w16"] + [(
+    "  constexpr int P = NW == 8 ? (R <= 2 ? 4 : (R == 4 ? 2 : 1)) : (R <= 4 ? 3 : 2);",
+    "  constexpr int P = NW == 8 ? (R <= 2 ? 4 : (R == 4 ? 2 : 1)) : 2;")]
