@@ -373,3 +373,21 @@ PATCHES["cn_w16"] = [("  if (V <= 256) return launch_cn<VARIANT, 2>(st, A, ptile
 PATCHES["cn_w16_p2"] = PATCHES["cn_w16"] + [(
     "  constexpr int P = NW == 8 ? (R <= 2 ? 4 : (R == 4 ? 2 : 1)) : (R <= 4 ? 3 : 2);",
     "  constexpr int P = NW == 8 ? (R <= 2 ? 4 : (R == 4 ? 2 : 1)) : 2;")]
+
+# k_consensus_p: two copies of the pair's histogram, lanes of even / odd rg
+# adding to their own (same-address atomics of a column's rows halve); the
+# readout adds the copies (integers: exact in any order)
+PATCHES["cp_hist2"] = [
+    ("  __shared__ __attribute__((aligned(16))) unsigned hb[NP * 32 * kHS];  // per pair: 32 columns",
+     "  __shared__ __attribute__((aligned(16))) unsigned hb[NP * 2 * 32 * kHS];  // per pair: 32 columns, 2 copies"),
+    ("      uint4* hz = reinterpret_cast<uint4*>(hb + pair * 32 * kHS);\n      constexpr int NW4 = 32 * kHS / 4;",
+     "      uint4* hz = reinterpret_cast<uint4*>(hb + pair * 2 * 32 * kHS);\n      constexpr int NW4 = 2 * 32 * kHS / 4;"),
+    ("      unsigned* hp = hb + pair * 32 * kHS;  // zeroed before the bracket barrier",
+     "      unsigned* hp = hb + pair * 2 * 32 * kHS;  // zeroed before the bracket barrier"),
+    ("          atomicAdd(hp + (col + c) * kHS + (k < w[c] ? k : w[c]), su);",
+     "          atomicAdd(hp + (rg & 1) * 32 * kHS + (col + c) * kHS + (k < w[c] ? k : w[c]), su);"),
+    ("        const uint4 a = *reinterpret_cast<const uint4*>(hc);\n        const uint4 b = *reinterpret_cast<const uint4*>(hc + 4);",
+     "        const uint4 a0 = *reinterpret_cast<const uint4*>(hc), a1 = *reinterpret_cast<const uint4*>(hc + 32 * kHS);\n"
+     "        const uint4 b0 = *reinterpret_cast<const uint4*>(hc + 4), b1 = *reinterpret_cast<const uint4*>(hc + 4 + 32 * kHS);\n"
+     "        const uint4 a = make_uint4(a0.x + a1.x, a0.y + a1.y, a0.z + a1.z, a0.w + a1.w);\n"
+     "        const uint4 b = make_uint4(b0.x + b1.x, b0.y + b1.y, b0.z + b1.z, b0.w + b1.w);")]
