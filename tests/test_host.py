@@ -441,3 +441,38 @@ def test_committed_counter_records_are_this_build():
         assert recs, path
         for r in recs:
             assert r.get("build_id") == bid, f"{os.path.relpath(path, ROOT)} {r['workload']}: {r.get('build_id')} != {bid}"
+
+
+def test_group_dividend_ratio_equals_per_run():
+    """run_simulations forms the dividend ratio of a whole batch in one pass of
+    the same elementwise ops (simulation_utils.py:95-107 restated): bitwise
+    the per-run results, on random stakes / dividends with zero stakes."""
+    import torch
+
+    from yuma_simulation._internal import simulation_utils as su
+    from yuma_simulation._internal.yumas import YumaConfig
+
+    g = torch.Generator().manual_seed(5)
+    S = torch.rand(40, 7, 3, generator=g)
+    S[3, 2, 1] = 0.0
+    Dn = torch.rand(40, 7, 3, generator=g)
+    cfg = YumaConfig()
+    whole = su._dividend_ratio(cfg, S, Dn)
+    for j in range(7):
+        one = su._dividend_ratio(cfg, S[:, j].contiguous(), Dn[:, j].contiguous())
+        assert np.array_equal(whole[:, j], one)
+
+
+def test_make_params_cache_matches_and_separates():
+    from yuma_simulation._internal.yumas import SimulationHyperparameters, YumaConfig, YumaParams
+
+    a = YumaConfig(yuma_params=YumaParams(bond_alpha=0.2))
+    b = YumaConfig(yuma_params=YumaParams(bond_alpha=0.2))
+    c = YumaConfig(simulation=SimulationHyperparameters(kappa=-0.0))
+    d = YumaConfig(simulation=SimulationHyperparameters(kappa=0.0))
+    pa = engine.make_params_cached(engine.VARIANT_YUMA4, a)
+    assert engine.make_params_cached(engine.VARIANT_YUMA4, b) is pa
+    assert bytes(pa) == bytes(engine.make_params(engine.VARIANT_YUMA4, a))
+    assert engine.make_params_cached(engine.VARIANT_YUMA3, a) is not pa
+    pc, pd = engine.make_params_cached(3, c), engine.make_params_cached(3, d)
+    assert pc is not pd and bytes(pc) == bytes(engine.make_params(3, c))

@@ -281,6 +281,40 @@ def make_params(variant: int, config, *, maxint: int = 2**64 - 1, reset_mode: in
     return p
 
 
+_PARAMS_CACHE: dict = {}
+_CONFIG_FIELDS = ("consensus_precision", "kappa", "bond_penalty", "bond_alpha", "alpha_low", "alpha_high",
+                  "capacity_alpha", "decay_rate", "liquid_alpha", "override_consensus_high",
+                  "override_consensus_low")
+
+
+def config_key(config) -> tuple:
+    """The values make_params reads from a config (repr: -0.0 and 0.0 differ)."""
+    return tuple(repr(getattr(config, f)) for f in _CONFIG_FIELDS)
+
+
+def make_params_cached(variant: int, config, *, reset_mode: int = RESET_NONE, reset_epoch=None,
+                       reset_index=None, n_miners: int | None = None, n_epochs: int | None = None,
+                       ckey: tuple | None = None) -> YumaParamsC:
+    """make_params memoised on every value it reads (the sheet builds 504
+    records from 36 distinct configurations). Plain int / None reset fields
+    only; anything else (a tensor-valued reset epoch) is built fresh. The
+    record is shared: callers copy it into the device tensor, never mutate it.
+    ckey: config_key(config), when the caller already has it."""
+    if not all(x is None or type(x) is int for x in (reset_epoch, reset_index)):
+        return make_params(variant, config, reset_mode=reset_mode, reset_epoch=reset_epoch,
+                           reset_index=reset_index, n_miners=n_miners, n_epochs=n_epochs)
+    key = (variant, reset_mode, reset_epoch, reset_index, n_miners, n_epochs,
+           config_key(config) if ckey is None else ckey)
+    p = _PARAMS_CACHE.get(key)
+    if p is None:
+        p = make_params(variant, config, reset_mode=reset_mode, reset_epoch=reset_epoch,
+                        reset_index=reset_index, n_miners=n_miners, n_epochs=n_epochs)
+        if len(_PARAMS_CACHE) > 65536:
+            _PARAMS_CACHE.clear()
+        _PARAMS_CACHE[key] = p
+    return p
+
+
 class _NoTruthValue(Exception):
     """reset_bonds_epoch is a tensor / array whose `epoch == e` has no truth value."""
 

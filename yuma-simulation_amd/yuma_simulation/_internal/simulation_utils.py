@@ -15,6 +15,9 @@ Drop-in for the reference's _internal/simulation_utils.py:
 
 from __future__ import annotations
 
+import gc
+from contextlib import contextmanager
+
 from collections import defaultdict
 from dataclasses import dataclass
 
@@ -62,21 +65,29 @@ class SimulationRun:
     yuma_config: YumaConfig
 
 
-def _dividends_per_1000_tao(case: BaseCase, config: YumaConfig, S: torch.Tensor,
-                            Dn: torch.Tensor) -> dict[str, list[float]]:
-    """Reference simulation_utils.py:48-49,95-107 on CPU tensors [E, V]: the
-    same torch ops (so the same fp32 roundings; a GPU `x / 1000.0` would be a
-    reciprocal multiply), then the Python-double ratio. This is O(E*V) output
-    formatting, not the hot path."""
+def _dividend_ratio(config: YumaConfig, S: torch.Tensor, Dn: torch.Tensor) -> np.ndarray:
+    """Reference simulation_utils.py:48-49,95-107 on CPU tensors of any shape
+    [..., V]: the same elementwise torch ops (so the same fp32 roundings; a GPU
+    `x / 1000.0` would be a reciprocal multiply), then the Python-double ratio
+    elementwise in IEEE double (the same bits as float(a) / float(b))."""
     stakes_tao = S * config.total_subnet_stake
     stakes_units = (stakes_tao / 1000.0).numpy().astype(np.float64)  # float(x.item()): exact widening
     E_i = config.validator_emission_ratio * Dn
     emission = (E_i * config.total_epoch_emission).numpy().astype(np.float64)
-    # the Python-double ratio, elementwise in IEEE double (the same bits)
     with np.errstate(divide="ignore", invalid="ignore"):
-        ratio = np.where(stakes_units > 1e-6, emission / stakes_units, 0.0)
-    cols = ratio.T.tolist()
+        return np.where(stakes_units > 1e-6, emission / stakes_units, 0.0)
+
+
+def _dividends_per_1000_tao(case: BaseCase, config: YumaConfig, S: torch.Tensor,
+                            Dn: torch.Tensor) -> dict[str, list[float]]:
+    """One run's dividend lists from [E, V] CPU tensors (O(E*V) output
+    formatting, not the hot path)."""
+    cols = _dividend_ratio(config, S, Dn).T.tolist()
     return {validator: cols[i] for i, validator in enumerate(case.validators)}
+
+
+def _reward_key(config: YumaConfig) -> tuple:
+    return (config.total_subnet_stake, config.validator_emission_ratio, config.total_epoch_emission)
 
 
 def run_simulations(runs: list[SimulationRun], *, want_bonds: bool = True,
@@ -84,6 +95,25 @@ def run_simulations(runs: list[SimulationRun], *, want_bonds: bool = True,
     """Run many simulations; runs that share (variant, E, V, M) go to the
     device as one batched engine call. Returns one (dividends, bonds, incentives)
     tuple per run, in order."""
+    # the result lists are thousands of fresh containers (the sheet: 1512
+    # dividend lists): the cyclic collector would sweep the process's whole
+    # heap several times while they are built; they hold no cycles
+    with _no_cyclic_gc():
+        return _run_simulations(runs, want_bonds, want_incentives)
+
+
+@contextmanager
+def _no_cyclic_gc():
+    enabled = gc.isenabled()
+    gc.disable()
+    try:
+        yield
+    finally:
+        if enabled:
+            gc.enable()
+
+
+def _run_simulations(runs: list[SimulationRun], want_bonds: bool, want_incentives: bool):
     groups: dict[tuple, list[int]] = defaultdict(list)
     packed = []
     for k, r in enumerate(runs):
@@ -93,25 +123,39 @@ def run_simulations(runs: list[SimulationRun], *, want_bonds: bool = True,
         groups[(variant,) + tuple(W.shape)].append(k)
 
     results: list = [None] * len(runs)
+    ckeys: dict[int, tuple] = {}  # per config object, for this call (the sheet shares 36 configs over 504 runs)
     for (variant, E, V, M), idx in groups.items():
         params = []
         for k in idx:
             r = runs[k]
             _, reset_mode, _, _ = packed[k]
-            params.append(engine.make_params(variant, r.yuma_config, reset_mode=reset_mode,
-                                             reset_epoch=r.case.reset_bonds_epoch,
-                                             reset_index=r.case.reset_bonds_index,
-                                             n_miners=M, n_epochs=E))
+            cfg = r.yuma_config
+            ck = ckeys.get(id(cfg))
+            if ck is None:
+                ck = ckeys[id(cfg)] = engine.config_key(cfg)
+            params.append(engine.make_params_cached(variant, cfg, reset_mode=reset_mode,
+                                                    reset_epoch=r.case.reset_bonds_epoch,
+                                                    reset_index=r.case.reset_bonds_index,
+                                                    n_miners=M, n_epochs=E, ckey=ck))
         W = torch.stack([packed[k][2] for k in idx], dim=1)  # [E, N, V, M]
         S = torch.stack([packed[k][3] for k in idx], dim=1)  # [E, N, V]
         res = engine.run(variant, params, W, S, want_hist=want_bonds)
         Dn = res.Dn.cpu()
         hist = res.B_hist.cpu() if want_bonds else None
         inc = res.I.cpu() if want_incentives else None
+        # the dividend ratio of the whole group in one pass of the same
+        # elementwise ops when its runs share the reward scalars (the sheet)
+        ratio = None
+        if len({_reward_key(runs[k].yuma_config) for k in idx}) == 1:
+            ratio = _dividend_ratio(runs[idx[0]].yuma_config, S.cpu(), Dn)  # [E, N, V]
         for j, k in enumerate(idx):
             r = runs[k]
             home = packed[k][2].device
-            div = _dividends_per_1000_tao(r.case, r.yuma_config, packed[k][3].cpu(), Dn[:, j])
+            if ratio is not None:
+                cols = ratio[:, j, :].T.tolist()
+                div = {validator: cols[i] for i, validator in enumerate(r.case.validators)}
+            else:
+                div = _dividends_per_1000_tao(r.case, r.yuma_config, packed[k][3].cpu(), Dn[:, j])
             bonds = [hist[e, j].clone().to(home) for e in range(E)] if want_bonds else []
             incentives = [inc[e, j].clone().to(home) for e in range(E)] if want_incentives else []
             results[k] = (div, bonds, incentives)
@@ -156,10 +200,12 @@ def _sheet_runs(cases: list[BaseCase], yuma_versions, hyper: SimulationHyperpara
     for case in cases:
         if len(case.validators) != 3:
             raise ValueError(f"Case '{case.name}' does not have exactly 3 validators.")
+    # one config per version, shared by every case's run (configs are read only)
+    configs = [YumaConfig(simulation=hyper, yuma_params=params) for _, params in yuma_versions]
     return [
-        SimulationRun(case, version, YumaConfig(simulation=hyper, yuma_params=params))
+        SimulationRun(case, version, cfg)
         for case in cases
-        for version, params in yuma_versions
+        for (version, _), cfg in zip(yuma_versions, configs)
     ]
 
 
@@ -183,12 +229,13 @@ def _sheet_frame(cases: list[BaseCase], yuma_versions, results) -> pd.DataFrame:
             for std in _STANDARDIZED:
                 row[f"{std} - {version}"] = by_std.get(std, 0.0)
         rows.append(row)
+    columns = ["Case"] + [f"{std} - {version}" for version, _ in yuma_versions for std in _STANDARDIZED]
+    if rows and list(rows[0]) == columns and all(list(r) == columns for r in rows):
+        # every row holds exactly these columns in this order (unique version
+        # names): the frame column by column, without the row-dict conversion
+        return pd.DataFrame({c: [r[c] for r in rows] for c in columns})
     df = pd.DataFrame(rows)
-    columns = ["Case"] + [
-        f"{std} - {version}" for version, _ in yuma_versions for std in _STANDARDIZED
-        if f"{std} - {version}" in df.columns
-    ]
-    return df[columns]
+    return df[[c for c in columns if c in df.columns]]
 
 
 def generate_total_dividends_table(
@@ -198,8 +245,9 @@ def generate_total_dividends_table(
 ) -> pd.DataFrame:
     """Total dividends per standardized validator and version (reference
     simulation_utils.py:319-381). All (case, version) runs are batched."""
-    runs = _sheet_runs(cases, yuma_versions, simulation_hyperparameters)
-    return _sheet_frame(cases, yuma_versions, run_simulations(runs, want_bonds=False, want_incentives=False))
+    with _no_cyclic_gc():
+        runs = _sheet_runs(cases, yuma_versions, simulation_hyperparameters)
+        return _sheet_frame(cases, yuma_versions, run_simulations(runs, want_bonds=False, want_incentives=False))
 
 
 def generate_total_dividends_tables(
@@ -211,12 +259,13 @@ def generate_total_dividends_tables(
     bond penalties, scripts/total_dividends_sheet_generator.py:14-59), with the
     runs of ALL tables packed into one engine call per variant (config c5:
     504 runs in five launches sequences instead of twenty)."""
-    per = [_sheet_runs(cases, yuma_versions, h) for h in simulation_hyperparameters]
-    flat = run_simulations([r for runs in per for r in runs], want_bonds=False, want_incentives=False)
-    out, k = [], 0
-    for runs in per:
-        out.append(_sheet_frame(cases, yuma_versions, flat[k:k + len(runs)]))
-        k += len(runs)
+    with _no_cyclic_gc():
+        per = [_sheet_runs(cases, yuma_versions, h) for h in simulation_hyperparameters]
+        flat = run_simulations([r for runs in per for r in runs], want_bonds=False, want_incentives=False)
+        out, k = [], 0
+        for runs in per:
+            out.append(_sheet_frame(cases, yuma_versions, flat[k:k + len(runs)]))
+            k += len(runs)
     return out
 
 
