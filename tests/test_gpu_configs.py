@@ -442,3 +442,33 @@ def test_sweep_bounded_update_and_its_fallbacks(case):
         np.testing.assert_array_equal(a.C[:, 1].cpu().numpy(), ref["C"])
         assert_close(a.Dn[:, 1].cpu().numpy(), ref["Dn"], what=f"{case} Dn")
         assert_close(a.B_final[1].cpu().numpy(), ref["B"][-1], what=f"{case} B_final")
+
+
+@pytest.mark.parametrize("V,M,variant", [(12, 100, engine.VARIANT_YUMA4), (10, 99, engine.VARIANT_YUMA3),
+                                         (40, 200, engine.VARIANT_YUMA1), (40, 130, engine.VARIANT_RUST)])
+def test_shared_input_multiclass_small_shapes(V, M, variant):
+    """The multi-class consensus / rank of shared-input sweeps (k_class_list,
+    k_consensus_mc, k_rank_mc) at the wave-owned row forms R = 1 (<= 16
+    validators) and R = 4 (<= 64), a last tile cut short (M not a multiple of
+    64) and M not a multiple of 4 (the scalar loads): bitwise the replicated
+    run, scenario 0 against the oracle."""
+    E, N = 7, 9
+    seed = 0x5EED0C1A + V + M
+    W1 = engine.synth_weights(seed, E, 1, V, M)
+    S1 = torch.from_numpy(synth.stakes(seed, E, 1, V, period=3)).to(W1.device)
+    cfgs = [YumaConfig(simulation=bench_sim(kappa=0.3 + 0.1 * (i % 3)),
+                       yuma_params=YumaParams(bond_alpha=0.05 + 0.03 * i, liquid_alpha=i % 2 == 1))
+            for i in range(N)]
+    params = [engine.make_params(variant, c) for c in cfgs]
+    a = engine.run(variant, params, W1, S1, want_hist=True, shared_inputs=True)
+    b = engine.run(variant, params, W1.expand(E, N, V, M).contiguous(), S1.expand(E, N, V).contiguous(),
+                   want_hist=True)
+    torch.cuda.synchronize()
+    for k in ("C", "Dn", "I", "B_hist", "B_final"):
+        assert torch.equal(getattr(a, k), getattr(b, k)), k
+    version = {engine.VARIANT_RUST: "Yuma 0 (subtensor)", engine.VARIANT_YUMA1: "Yuma 1 (paper)",
+               engine.VARIANT_YUMA3: "Yuma 3 (Rhef)", engine.VARIANT_YUMA4: "Yuma 4 (Rhef+relative bonds)"}[variant]
+    ref = orc.run(version, W1[:, 0].cpu().numpy(), S1[:, 0].cpu().numpy(), cfgs[0])
+    np.testing.assert_array_equal(a.C[:, 0].cpu().numpy(), ref["C"])
+    assert_close(a.Dn[:, 0].cpu().numpy(), ref["Dn"], what="Dn")
+    assert_close(a.B_hist[:, 0].cpu().numpy(), ref["B"], what="B")
