@@ -476,3 +476,73 @@ def test_make_params_cache_matches_and_separates():
     assert engine.make_params_cached(engine.VARIANT_YUMA3, a) is not pa
     pc, pd = engine.make_params_cached(3, c), engine.make_params_cached(3, d)
     assert pc is not pd and bytes(pc) == bytes(engine.make_params(3, c))
+
+
+def test_prefix_totals_equal_list_sums():
+    """The sheet's totals path (simulation_utils._prefix_total over numpy's
+    sequential running sums) gives the bits of summing the per-epoch lists
+    with Python's sum() (charts_utils.py:19 restated): prefixes shorter, equal
+    and longer than the run, an empty and a negative slice, -0.0 terms."""
+    from yuma_simulation._internal import simulation_utils as su
+
+    rng = np.random.default_rng(11)
+    E = 40
+    x = rng.random((E, 3)) * 10.0 ** rng.integers(-8, 8, (E, 3))
+    x[:, 2] = -0.0
+    x[5, 1] = 0.0
+    cs = np.cumsum(x, axis=0)
+    cols = x.T.tolist()
+    for n in (0, 1, 7, 39, 40, 55, -3):
+        got = su._prefix_total(cs, E, n)
+        want = [sum(c[:n]) for c in cols]
+        assert [type(g) for g in got] == [type(w) for w in want], n
+        assert [repr(g) for g in got] == [repr(w) for w in want], n
+
+
+def test_sheet_frame_block_equals_row_frame(capsys):
+    """_sheet_frame_totals' float64 block equals the row-dict frame (same
+    columns, dtypes, CSV text and zero-base warnings) on the reference's
+    cases, and keeps the row form for int totals (an empty epoch range)."""
+    from yuma_simulation._internal import simulation_utils as su
+
+    vers = su.sheet_yuma_versions()
+    rng = np.random.default_rng(3)
+    for zero in (False, True):
+        tots = []
+        for case in C.cases:
+            for _ in vers:
+                t = {v: float(rng.random()) for v in case.validators}
+                if zero:
+                    t[case.base_validator] = 0.0
+                tots.append(t)
+        a = su._sheet_frame_totals(C.cases, vers, tots)
+        wa = capsys.readouterr().out
+        rows = []
+        it = iter(tots)
+        for case in C.cases:
+            row = {"Case": case.name}
+            std_of = dict(zip(case.validators, su._STANDARDIZED))
+            for version, _ in vers:
+                t = next(it)
+                if t.get(case.base_validator) in (None, 0.0):
+                    print(f"Warning: Base validator '{case.base_validator}' has zero or missing total dividends.")
+                by_std = {std_of[v]: t.get(v, 0.0) for v in case.validators}
+                for std in su._STANDARDIZED:
+                    row[f"{std} - {version}"] = by_std.get(std, 0.0)
+            rows.append(row)
+        b = pd_frame(rows)
+        wb = capsys.readouterr().out
+        assert list(a.columns) == list(b.columns) and a.dtypes.equals(b.dtypes)
+        assert a.to_csv(index=False, float_format="%.6f") == b.to_csv(index=False, float_format="%.6f")
+        assert a.to_csv(index=False) == b.to_csv(index=False)
+        assert wa == wb and (zero == (len(wa) > 0))
+    ints = [{v: 0 for v in case.validators} for case in C.cases for _ in vers]
+    c = su._sheet_frame_totals(C.cases, vers, ints)
+    capsys.readouterr()
+    assert str(c.dtypes.iloc[1]) == "int64"
+
+
+def pd_frame(rows):
+    import pandas as pd
+
+    return pd.DataFrame(rows)

@@ -113,7 +113,23 @@ def _no_cyclic_gc():
             gc.enable()
 
 
-def _run_simulations(runs: list[SimulationRun], want_bonds: bool, want_incentives: bool):
+def _prefix_total(cs: np.ndarray, E: int, n: int):
+    """sum(lst[:n]) of an E-entry list of floats from the running sums cs
+    [E, V] of its values: Python's left-to-right double sum from int 0, i.e.
+    the prefix's running sum (+0.0 turns a -0.0 into the +0.0 that 0 + -0.0
+    gives) or the int 0 of an empty slice."""
+    k = len(range(E)[:n])
+    if k == 0:
+        return [0] * cs.shape[1]
+    return (cs[k - 1] + 0.0).tolist()
+
+
+def _run_simulations(runs: list[SimulationRun], want_bonds: bool, want_incentives: bool,
+                     totals: bool = False):
+    """totals: each run's dividends as {validator: sum of its first
+    case.num_epochs per-epoch values} (the sheet's totals, the same bits as
+    summing the lists) instead of the per-epoch lists, with no bonds or
+    incentives."""
     groups: dict[tuple, list[int]] = defaultdict(list)
     packed = []
     for k, r in enumerate(runs):
@@ -148,6 +164,17 @@ def _run_simulations(runs: list[SimulationRun], want_bonds: bool, want_incentive
         ratio = None
         if len({_reward_key(runs[k].yuma_config) for k in idx}) == 1:
             ratio = _dividend_ratio(runs[idx[0]].yuma_config, S.cpu(), Dn)  # [E, N, V]
+        if totals:
+            csum = np.cumsum(ratio, axis=0) if ratio is not None else None  # sequential, as sum()
+            for j, k in enumerate(idx):
+                r = runs[k]
+                if csum is not None:
+                    cs = csum[:, j, :]
+                else:
+                    cs = np.cumsum(_dividend_ratio(r.yuma_config, packed[k][3].cpu(), Dn[:, j]), axis=0)
+                tot = _prefix_total(cs, E, r.case.num_epochs)
+                results[k] = ({validator: tot[i] for i, validator in enumerate(r.case.validators)}, None, None)
+            continue
         for j, k in enumerate(idx):
             r = runs[k]
             home = packed[k][2].device
@@ -210,30 +237,52 @@ def _sheet_runs(cases: list[BaseCase], yuma_versions, hyper: SimulationHyperpara
 
 
 def _sheet_frame(cases: list[BaseCase], yuma_versions, results) -> pd.DataFrame:
-    """Rows of the dividend sheet from the runs' results, in _sheet_runs order
-    (reference simulation_utils.py:341-381)."""
+    """Rows of the dividend sheet from the runs' results (dividend lists), in
+    _sheet_runs order (reference simulation_utils.py:341-381)."""
     results = iter(results)
-    rows: list[dict[str, object]] = []
+    totals = []
     for case in cases:
-        mapping = dict(zip(case.validators, _STANDARDIZED))
-        row: dict[str, object] = {"Case": case.name}
-        for version, _ in yuma_versions:
+        for _ in yuma_versions:
             dividends, _, _ = next(results)
-            totals, _ = _calculate_total_dividends(
-                validators=case.validators,
-                dividends_per_validator=dividends,
-                base_validator=case.base_validator,
-                num_epochs=case.num_epochs,
-            )
-            by_std = {mapping[v]: totals.get(v, 0.0) for v in case.validators}
-            for std in _STANDARDIZED:
-                row[f"{std} - {version}"] = by_std.get(std, 0.0)
-        rows.append(row)
+            n = case.num_epochs
+            totals.append({v: sum(dividends.get(v, [])[:n]) for v in case.validators})
+    return _sheet_frame_totals(cases, yuma_versions, totals)
+
+
+def _sheet_frame_totals(cases: list[BaseCase], yuma_versions, totals) -> pd.DataFrame:
+    """The sheet from each run's total dividend per validator (the totals of
+    _calculate_total_dividends, reference charts_utils.py:15-45, with its
+    zero-base warning; its percentage differences are not part of the sheet).
+    Float totals go into one float64 block: one frame construction instead
+    of one column at a time (the same values, dtypes and CSV text); otherwise
+    (the int 0 of an empty epoch range, no cases, repeated version names) the
+    frame is built from row dicts."""
+    nv = len(yuma_versions)
     columns = ["Case"] + [f"{std} - {version}" for version, _ in yuma_versions for std in _STANDARDIZED]
-    if rows and list(rows[0]) == columns and all(list(r) == columns for r in rows):
-        # every row holds exactly these columns in this order (unique version
-        # names): the frame column by column, without the row-dict conversion
-        return pd.DataFrame({c: [r[c] for r in rows] for c in columns})
+    block = bool(cases) and len(set(columns)) == len(columns) and all(
+        type(x) is float for t in totals for x in t.values())
+    vals = np.zeros((len(cases), 3 * nv), dtype=np.float64) if block else None
+    rows: list[dict[str, object]] = []
+    it = iter(totals)
+    for ci, case in enumerate(cases):
+        std_of = dict(zip(case.validators, _STANDARDIZED))
+        row: dict[str, object] = {"Case": case.name}
+        for vi, (version, _) in enumerate(yuma_versions):
+            tot = next(it)
+            base = tot.get(case.base_validator)
+            if base is None or base == 0.0:
+                print(f"Warning: Base validator '{case.base_validator}' has zero or missing total dividends.")
+            by_std = {std_of[v]: tot.get(v, 0.0) for v in case.validators}
+            for si, std in enumerate(_STANDARDIZED):
+                if block:
+                    vals[ci, 3 * vi + si] = by_std.get(std, 0.0)
+                else:
+                    row[f"{std} - {version}"] = by_std.get(std, 0.0)
+        rows.append(row)
+    if block:
+        df = pd.DataFrame(vals, columns=columns[1:])
+        df.insert(0, "Case", [case.name for case in cases])
+        return df
     df = pd.DataFrame(rows)
     return df[[c for c in columns if c in df.columns]]
 
@@ -247,7 +296,7 @@ def generate_total_dividends_table(
     simulation_utils.py:319-381). All (case, version) runs are batched."""
     with _no_cyclic_gc():
         runs = _sheet_runs(cases, yuma_versions, simulation_hyperparameters)
-        return _sheet_frame(cases, yuma_versions, run_simulations(runs, want_bonds=False, want_incentives=False))
+        return _sheet_frame_totals(cases, yuma_versions, [d for d, _, _ in _run_simulations(runs, False, False, totals=True)])
 
 
 def generate_total_dividends_tables(
@@ -261,10 +310,10 @@ def generate_total_dividends_tables(
     504 runs in five launches sequences instead of twenty)."""
     with _no_cyclic_gc():
         per = [_sheet_runs(cases, yuma_versions, h) for h in simulation_hyperparameters]
-        flat = run_simulations([r for runs in per for r in runs], want_bonds=False, want_incentives=False)
+        flat = [d for d, _, _ in _run_simulations([r for runs in per for r in runs], False, False, totals=True)]
         out, k = [], 0
         for runs in per:
-            out.append(_sheet_frame(cases, yuma_versions, flat[k:k + len(runs)]))
+            out.append(_sheet_frame_totals(cases, yuma_versions, flat[k:k + len(runs)]))
             k += len(runs)
     return out
 
