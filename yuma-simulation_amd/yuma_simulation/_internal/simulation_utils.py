@@ -140,6 +140,10 @@ def _run_simulations(runs: list[SimulationRun], want_bonds: bool, want_incentive
 
     results: list = [None] * len(runs)
     ckeys: dict[int, tuple] = {}  # per config object, for this call (the sheet shares 36 configs over 504 runs)
+    # every group's engine run is queued before the first result is copied
+    # back, so the device works through the later groups while the host
+    # formats the earlier ones (the sheet: five groups)
+    launched = []
     for (variant, E, V, M), idx in groups.items():
         params = []
         for k in idx:
@@ -155,7 +159,8 @@ def _run_simulations(runs: list[SimulationRun], want_bonds: bool, want_incentive
                                                     n_miners=M, n_epochs=E, ckey=ck))
         W = torch.stack([packed[k][2] for k in idx], dim=1)  # [E, N, V, M]
         S = torch.stack([packed[k][3] for k in idx], dim=1)  # [E, N, V]
-        res = engine.run(variant, params, W, S, want_hist=want_bonds)
+        launched.append((E, idx, S, engine.run(variant, params, W, S, want_hist=want_bonds)))
+    for E, idx, S, res in launched:
         Dn = res.Dn.cpu()
         hist = res.B_hist.cpu() if want_bonds else None
         inc = res.I.cpu() if want_incentives else None
