@@ -113,6 +113,33 @@ def _no_cyclic_gc():
             gc.enable()
 
 
+# stacked device inputs of small run groups, by the identity of their cases'
+# packed inputs (built once per case and read only, cases.packed_inputs): the
+# sheet restacks and uploads the same five groups on every call otherwise
+_GROUP_INPUTS: dict = {}
+_GROUP_INPUTS_MAX_ELEMS = 1 << 20  # per run; larger groups are stacked per call
+
+
+def _group_inputs(packed: list, elems: int):
+    """(W [E,N,V,M] and S [E,N,V] on the engine's device, S on the host)."""
+    src = tuple(t for p in packed for t in (p[2], p[3]))
+    key = tuple(id(t) for t in src)
+    if elems <= _GROUP_INPUTS_MAX_ELEMS:
+        ent = _GROUP_INPUTS.get(key)
+        if ent is not None and all(a is b for a, b in zip(ent[0], src)):
+            return ent[1:]
+    W = torch.stack([p[2] for p in packed], dim=1)
+    S_host = torch.stack([p[3] for p in packed], dim=1).cpu()
+    dev = engine.device()
+    out = (W.to(device=dev, dtype=torch.float32).contiguous(),
+           S_host.to(device=dev, dtype=torch.float32).contiguous(), S_host)
+    if elems <= _GROUP_INPUTS_MAX_ELEMS:
+        if len(_GROUP_INPUTS) >= 64:
+            _GROUP_INPUTS.clear()
+        _GROUP_INPUTS[key] = (src,) + out
+    return out
+
+
 def _prefix_total(cs: np.ndarray, E: int, n: int):
     """sum(lst[:n]) of an E-entry list of floats from the running sums cs
     [E, V] of its values: Python's left-to-right double sum from int 0, i.e.
@@ -157,10 +184,9 @@ def _run_simulations(runs: list[SimulationRun], want_bonds: bool, want_incentive
                                                     reset_epoch=r.case.reset_bonds_epoch,
                                                     reset_index=r.case.reset_bonds_index,
                                                     n_miners=M, n_epochs=E, ckey=ck))
-        W = torch.stack([packed[k][2] for k in idx], dim=1)  # [E, N, V, M]
-        S = torch.stack([packed[k][3] for k in idx], dim=1)  # [E, N, V]
-        launched.append((E, idx, S, engine.run(variant, params, W, S, want_hist=want_bonds)))
-    for E, idx, S, res in launched:
+        W, S, S_host = _group_inputs([packed[k] for k in idx], E * V * M)
+        launched.append((E, V, idx, S_host, engine.run(variant, params, W, S, want_hist=want_bonds)))
+    for E, V, idx, S, res in launched:
         Dn = res.Dn.cpu()
         hist = res.B_hist.cpu() if want_bonds else None
         inc = res.I.cpu() if want_incentives else None
@@ -168,16 +194,19 @@ def _run_simulations(runs: list[SimulationRun], want_bonds: bool, want_incentive
         # elementwise ops when its runs share the reward scalars (the sheet)
         ratio = None
         if len({_reward_key(runs[k].yuma_config) for k in idx}) == 1:
-            ratio = _dividend_ratio(runs[idx[0]].yuma_config, S.cpu(), Dn)  # [E, N, V]
+            ratio = _dividend_ratio(runs[idx[0]].yuma_config, S, Dn)  # [E, N, V]
         if totals:
-            csum = np.cumsum(ratio, axis=0) if ratio is not None else None  # sequential, as sum()
+            if ratio is not None:  # the group's prefix sums in one gather (the rows _prefix_total takes)
+                csum = np.cumsum(ratio, axis=0)  # sequential, as sum()
+                ks = [len(range(E)[:runs[k].case.num_epochs]) for k in idx]
+                rows = (csum[[max(x - 1, 0) for x in ks], range(len(idx)), :] + 0.0).tolist()
             for j, k in enumerate(idx):
                 r = runs[k]
-                if csum is not None:
-                    cs = csum[:, j, :]
+                if ratio is not None:
+                    tot = rows[j] if ks[j] > 0 else [0] * V
                 else:
                     cs = np.cumsum(_dividend_ratio(r.yuma_config, packed[k][3].cpu(), Dn[:, j]), axis=0)
-                tot = _prefix_total(cs, E, r.case.num_epochs)
+                    tot = _prefix_total(cs, E, r.case.num_epochs)
                 results[k] = ({validator: tot[i] for i, validator in enumerate(r.case.validators)}, None, None)
             continue
         for j, k in enumerate(idx):
