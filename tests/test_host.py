@@ -515,7 +515,8 @@ def test_sheet_frame_block_equals_row_frame(capsys):
                 if zero:
                     t[case.base_validator] = 0.0
                 tots.append(t)
-        a = su._sheet_frame_totals(C.cases, vers, tots)
+        lists = [[t[v] for v in C.cases[i // len(vers)].validators] for i, t in enumerate(tots)]
+        a = su._sheet_frame_totals(C.cases, vers, lists)
         wa = capsys.readouterr().out
         rows = []
         it = iter(tots)
@@ -536,7 +537,7 @@ def test_sheet_frame_block_equals_row_frame(capsys):
         assert a.to_csv(index=False, float_format="%.6f") == b.to_csv(index=False, float_format="%.6f")
         assert a.to_csv(index=False) == b.to_csv(index=False)
         assert wa == wb and (zero == (len(wa) > 0))
-    ints = [{v: 0 for v in case.validators} for case in C.cases for _ in vers]
+    ints = [[0 for v in case.validators] for case in C.cases for _ in vers]
     c = su._sheet_frame_totals(C.cases, vers, ints)
     capsys.readouterr()
     assert str(c.dtypes.iloc[1]) == "int64"

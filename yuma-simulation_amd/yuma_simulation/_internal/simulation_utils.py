@@ -153,10 +153,10 @@ def _prefix_total(cs: np.ndarray, E: int, n: int):
 
 def _run_simulations(runs: list[SimulationRun], want_bonds: bool, want_incentives: bool,
                      totals: bool = False):
-    """totals: each run's dividends as {validator: sum of its first
-    case.num_epochs per-epoch values} (the sheet's totals, the same bits as
-    summing the lists) instead of the per-epoch lists, with no bonds or
-    incentives."""
+    """totals: each run's dividends as the sums of its first case.num_epochs
+    per-epoch values, one per validator in case.validators order (the sheet's
+    totals, the same bits as summing the lists) instead of the per-epoch
+    lists, with no bonds or incentives."""
     groups: dict[tuple, list[int]] = defaultdict(list)
     packed = []
     for k, r in enumerate(runs):
@@ -207,7 +207,7 @@ def _run_simulations(runs: list[SimulationRun], want_bonds: bool, want_incentive
                 else:
                     cs = np.cumsum(_dividend_ratio(r.yuma_config, packed[k][3].cpu(), Dn[:, j]), axis=0)
                     tot = _prefix_total(cs, E, r.case.num_epochs)
-                results[k] = ({validator: tot[i] for i, validator in enumerate(r.case.validators)}, None, None)
+                results[k] = (tot, None, None)
             continue
         for j, k in enumerate(idx):
             r = runs[k]
@@ -279,45 +279,56 @@ def _sheet_frame(cases: list[BaseCase], yuma_versions, results) -> pd.DataFrame:
         for _ in yuma_versions:
             dividends, _, _ = next(results)
             n = case.num_epochs
-            totals.append({v: sum(dividends.get(v, [])[:n]) for v in case.validators})
+            totals.append([sum(dividends.get(v, [])[:n]) for v in case.validators])
     return _sheet_frame_totals(cases, yuma_versions, totals)
 
 
 def _sheet_frame_totals(cases: list[BaseCase], yuma_versions, totals) -> pd.DataFrame:
-    """The sheet from each run's total dividend per validator (the totals of
-    _calculate_total_dividends, reference charts_utils.py:15-45, with its
-    zero-base warning; its percentage differences are not part of the sheet).
-    Float totals go into one float64 block: one frame construction instead
-    of one column at a time (the same values, dtypes and CSV text); otherwise
-    (the int 0 of an empty epoch range, no cases, repeated version names) the
-    frame is built from row dicts."""
+    """The sheet from each run's total dividends (one per validator, in
+    case.validators order): the totals of _calculate_total_dividends,
+    reference charts_utils.py:15-45, with its zero-base warning (its
+    percentage differences are not part of the sheet). With three distinct
+    validators per case (validator i is standardised name i) and float totals
+    the rows go into one float64 block: one frame construction instead of one
+    column at a time (the same values, dtypes and CSV text); otherwise (the
+    int 0 of an empty epoch range, no cases, repeated names) the frame is
+    built from row dicts."""
     nv = len(yuma_versions)
     columns = ["Case"] + [f"{std} - {version}" for version, _ in yuma_versions for std in _STANDARDIZED]
-    block = bool(cases) and len(set(columns)) == len(columns) and all(
-        type(x) is float for t in totals for x in t.values())
-    vals = np.zeros((len(cases), 3 * nv), dtype=np.float64) if block else None
-    rows: list[dict[str, object]] = []
+    block = (bool(cases) and len(set(columns)) == len(columns)
+             and all(len(set(c.validators)) == len(c.validators) == 3 for c in cases)
+             and all(type(x) is float for t in totals for x in t))
+    warn = "Warning: Base validator '{}' has zero or missing total dividends."
     it = iter(totals)
-    for ci, case in enumerate(cases):
-        std_of = dict(zip(case.validators, _STANDARDIZED))
-        row: dict[str, object] = {"Case": case.name}
-        for vi, (version, _) in enumerate(yuma_versions):
-            tot = next(it)
-            base = tot.get(case.base_validator)
-            if base is None or base == 0.0:
-                print(f"Warning: Base validator '{case.base_validator}' has zero or missing total dividends.")
-            by_std = {std_of[v]: tot.get(v, 0.0) for v in case.validators}
-            for si, std in enumerate(_STANDARDIZED):
-                if block:
-                    vals[ci, 3 * vi + si] = by_std.get(std, 0.0)
-                else:
-                    row[f"{std} - {version}"] = by_std.get(std, 0.0)
-        rows.append(row)
     if block:
-        df = pd.DataFrame(vals, columns=columns[1:])
+        rows = []
+        for case in cases:
+            vs, bv = case.validators, case.base_validator
+            bi = vs.index(bv) if bv in vs else None
+            row: list = []
+            for _ in range(nv):
+                tot = next(it)
+                if bi is None or tot[bi] == 0.0:
+                    print(warn.format(bv))
+                row += tot
+            rows.append(row)
+        df = pd.DataFrame(np.array(rows, dtype=np.float64), columns=columns[1:])
         df.insert(0, "Case", [case.name for case in cases])
         return df
-    df = pd.DataFrame(rows)
+    drows: list[dict[str, object]] = []
+    for case in cases:
+        std_of = dict(zip(case.validators, _STANDARDIZED))
+        drow: dict[str, object] = {"Case": case.name}
+        for version, _ in yuma_versions:
+            tot = dict(zip(case.validators, next(it)))
+            base = tot.get(case.base_validator)
+            if base is None or base == 0.0:
+                print(warn.format(case.base_validator))
+            by_std = {std_of[v]: tot.get(v, 0.0) for v in case.validators}
+            for std in _STANDARDIZED:
+                drow[f"{std} - {version}"] = by_std.get(std, 0.0)
+        drows.append(drow)
+    df = pd.DataFrame(drows)
     return df[[c for c in columns if c in df.columns]]
 
 
