@@ -173,17 +173,23 @@ def _run_simulations(runs: list[SimulationRun], want_bonds: bool, want_incentive
     launched = []
     for (variant, E, V, M), idx in groups.items():
         params = []
+        local: dict = {}  # (config object, reset fields) -> record, within the group
         for k in idx:
             r = runs[k]
-            _, reset_mode, _, _ = packed[k]
+            reset_mode = packed[k][1]
             cfg = r.yuma_config
-            ck = ckeys.get(id(cfg))
-            if ck is None:
-                ck = ckeys[id(cfg)] = engine.config_key(cfg)
-            params.append(engine.make_params_cached(variant, cfg, reset_mode=reset_mode,
-                                                    reset_epoch=r.case.reset_bonds_epoch,
-                                                    reset_index=r.case.reset_bonds_index,
-                                                    n_miners=M, n_epochs=E, ckey=ck))
+            re_, ri_ = r.case.reset_bonds_epoch, r.case.reset_bonds_index
+            lk = (id(cfg), reset_mode, re_, ri_) if type(re_) in (int, type(None)) and type(ri_) in (int, type(None)) else None
+            rec = local.get(lk) if lk is not None else None
+            if rec is None:
+                ck = ckeys.get(id(cfg))
+                if ck is None:
+                    ck = ckeys[id(cfg)] = engine.config_key(cfg)
+                rec = engine.make_params_cached(variant, cfg, reset_mode=reset_mode, reset_epoch=re_,
+                                                reset_index=ri_, n_miners=M, n_epochs=E, ckey=ck)
+                if lk is not None:
+                    local[lk] = rec
+            params.append(rec)
         W, S, S_host = _group_inputs([packed[k] for k in idx], E * V * M)
         launched.append((E, V, idx, S_host, engine.run(variant, params, W, S, want_hist=want_bonds)))
     for E, V, idx, S, res in launched:
