@@ -117,11 +117,12 @@ def _no_cyclic_gc():
 # packed inputs (built once per case and read only, cases.packed_inputs): the
 # sheet restacks and uploads the same five groups on every call otherwise
 _GROUP_INPUTS: dict = {}
-_GROUP_INPUTS_MAX_ELEMS = 1 << 20  # per run; larger groups are stacked per call
+_GROUP_INPUTS_MAX_ELEMS = 1 << 22  # W elements of a whole group; larger groups are stacked per call
 
 
 def _group_inputs(packed: list, elems: int):
-    """(W [E,N,V,M] and S [E,N,V] on the engine's device, S on the host)."""
+    """(W [E,N,V,M] and S [E,N,V] on the engine's device, S on the host);
+    elems: the group's W elements."""
     src = tuple(t for p in packed for t in (p[2], p[3]))
     key = tuple(id(t) for t in src)
     if elems <= _GROUP_INPUTS_MAX_ELEMS:
@@ -138,6 +139,9 @@ def _group_inputs(packed: list, elems: int):
             _GROUP_INPUTS.clear()
         _GROUP_INPUTS[key] = (src,) + out
     return out
+
+
+_PLAIN = (int, type(None))
 
 
 def _prefix_total(cs: np.ndarray, E: int, n: int):
@@ -179,8 +183,9 @@ def _run_simulations(runs: list[SimulationRun], want_bonds: bool, want_incentive
             reset_mode = packed[k][1]
             cfg = r.yuma_config
             re_, ri_ = r.case.reset_bonds_epoch, r.case.reset_bonds_index
-            lk = (id(cfg), reset_mode, re_, ri_) if type(re_) in (int, type(None)) and type(ri_) in (int, type(None)) else None
-            rec = local.get(lk) if lk is not None else None
+            plain = type(re_) in _PLAIN and type(ri_) in _PLAIN  # make_params_cached's memo rule
+            lk = (id(cfg), reset_mode, re_, ri_) if plain else None
+            rec = local.get(lk) if plain else None
             if rec is None:
                 ck = ckeys.get(id(cfg))
                 if ck is None:
@@ -190,7 +195,7 @@ def _run_simulations(runs: list[SimulationRun], want_bonds: bool, want_incentive
                 if lk is not None:
                     local[lk] = rec
             params.append(rec)
-        W, S, S_host = _group_inputs([packed[k] for k in idx], E * V * M)
+        W, S, S_host = _group_inputs([packed[k] for k in idx], E * V * M * len(idx))
         launched.append((E, V, idx, S_host, engine.run(variant, params, W, S, want_hist=want_bonds)))
     for E, V, idx, S, res in launched:
         Dn = res.Dn.cpu()
