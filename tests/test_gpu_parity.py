@@ -105,6 +105,30 @@ def test_sheet_all_tables_batched_and_scripts(tmp_path):
             assert hashlib.md5(f.read()).hexdigest() == meta["csv_md5"][os.path.basename(path)]
 
 
+def test_sheet_totals_with_mixed_reward_scalars():
+    """Tables whose hyperparameters differ in the reward scalars (subnet
+    stake, emission) land in one engine group with no shared dividend ratio:
+    the sheet's totals path then sums each run's own ratios. Every table
+    equals the frame built from the runs' per-epoch dividend lists
+    (reference simulation_utils.py:341-381 over run_simulation's lists), and
+    the same tables one call at a time."""
+    from yuma_simulation._internal import simulation_utils as su
+
+    versions = su.sheet_yuma_versions()
+    hypers = [Y.SimulationHyperparameters(bond_penalty=0.5),
+              Y.SimulationHyperparameters(bond_penalty=0.5, total_subnet_stake=3.5e5),
+              Y.SimulationHyperparameters(bond_penalty=0.99, total_epoch_emission=37.0,
+                                          validator_emission_ratio=0.3)]
+    frames = su.generate_total_dividends_tables(cases, versions, hypers)
+    for h, df in zip(hypers, frames):
+        runs = su._sheet_runs(cases, versions, h)
+        lists = su._sheet_frame(cases, versions, su.run_simulations(runs, want_bonds=False, want_incentives=False))
+        one = su.generate_total_dividends_table(cases, versions, h)
+        for other in (lists, one):
+            assert list(df.columns) == list(other.columns) and df.dtypes.equals(other.dtypes)
+            assert df.to_csv(index=False) == other.to_csv(index=False)
+
+
 def test_sheet_runs_per_epoch(golden):
     """Every (beta, case, version) run: consensus exact, dividends / bonds /
     incentives within tolerance; all 504 runs go through batched launches."""
